@@ -1,0 +1,160 @@
+/*
+ * phgpu.h -- C-ABI of the MI355X-native progressive-hedging hot path.
+ *
+ * One handle holds one rank's local scenarios: a CSR sparsity pattern shared by all
+ * of them and per-scenario coefficient / bound / objective arrays.  The library
+ * replaces, for all local scenarios at once:
+ *
+ *   - SPOpt.solve_loop / solve_one        mpisppy/spopt.py:226-307 / 85-223
+ *       (one LP/QP per scenario through Pyomo's SolverFactory plugin .solve(),
+ *        spopt.py:165-172; results fields spopt.py:175-206)      -> phgpu_solve
+ *   - PHBase.attach_PH_to_objective terms  mpisppy/phbase.py:617-699
+ *       (W_on * W.x + prox_on * rho/2 (x - xbar)^2)                -> phgpu_set_ph_state
+ *   - _Compute_Xbar local sums             mpisppy/phbase.py:27-87  -> phgpu_ph_reduce
+ *   - Update_W + convergence_diff          mpisppy/phbase.py:293-343 -> phgpu_ph_update
+ *   - SPOpt.Ebound / Eobjective / _update_E1 / feas_prob local sums
+ *                                          mpisppy/spopt.py:310-439 -> phgpu_expectations
+ *
+ * The cross-rank sums (the per-node MPI Allreduce of phbase.py:83-87 and the
+ * ROOT-comm Allreduce of phbase.py:341) are done by the caller (RCCL all-reduce of
+ * the node buffer) between phgpu_ph_reduce and phgpu_ph_update.
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative code on error; the text of
+ *     the last error of the calling thread is available from phgpu_last_error.
+ *   - "host" pointers are read during the call only.  "device" pointers are HIP
+ *     device pointers (e.g. torch.Tensor.data_ptr() of a cuda tensor) owned by the
+ *     caller; the library owns only the workspace it allocates in phgpu_create and
+ *     frees in phgpu_destroy.
+ *   - Per-scenario arrays are scenario-fastest: element (k, s) of a k-indexed
+ *     quantity lives at [k * S + s]  (coalesced: 64 lanes = 64 scenarios).
+ *   - All work is ordered on the given hipStream_t (NULL = default stream); no call
+ *     synchronises the device except phgpu_create / phgpu_destroy.
+ *   - A handle is used by one host thread; it is not re-entrant; one process per GPU.
+ *   - The problem is stored as a minimisation; a maximise model is negated by the
+ *     caller (phbase.py:696-699 subtracts the PH term for max, which is the same).
+ */
+#ifndef PHGPU_H
+#define PHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct phgpu_state* phgpu_handle;
+
+/* Per-scenario solve status (mapped to _mpisppy_data.scenario_feasible and the
+ * termination_condition checks of spopt.py:175-194). */
+enum {
+    PHGPU_OPTIMAL = 0,
+    PHGPU_ITER_LIMIT = 1,
+    PHGPU_PRIMAL_INFEASIBLE = 2,
+    PHGPU_DUAL_INFEASIBLE = 3
+};
+
+/* Solver options (the iter0_solver_options / iterk_solver_options dicts of
+ * phbase.py:273-274 become these fields). */
+typedef struct {
+    double eps_rel;        /* relative KKT tolerance (primal, dual, gap)      [1e-10] */
+    double eps_abs;        /* absolute KKT tolerance                          [1e-12] */
+    int32_t max_iter;      /* PDHG iteration cap per scenario                 [100000] */
+    int32_t check_every;   /* KKT / restart check period (iterations)         [64] */
+    double gamma;          /* Halpern reflection coefficient in [0, 1]         [1.0] */
+    double beta_sufficient;/* restart if r <= beta_suff * r_restart           [0.2] */
+    double beta_necessary; /* ... or r <= beta_nec * r_restart and no progress [0.8] */
+    double eta_frac;       /* step = eta_frac / ||A_scaled||_2                [0.998] */
+    double omega0;         /* initial primal weight (<= 0: keep previous)     [1.0] */
+    int32_t keep_omega;    /* 1: carry the primal weight across solves         [1] */
+    int32_t reserved;
+} phgpu_options;
+
+/* Fill *opt with the defaults shown above. */
+int phgpu_default_options(phgpu_options* opt);
+
+/* Create a handle for S local scenarios sharing one CSR pattern.
+ * Replaces: SPOpt._create_solvers / set_instance (spopt.py:839-903) and the
+ * nonant index bookkeeping of SPBase._attach_nlens / _attach_nonant_indices
+ * (spbase.py:293-320).
+ *   row_ptr[m+1], col_idx[nnz]          host, the shared pattern
+ *   nonant_col[nn]                      host, column of flat nonant k (node-list
+ *                                       order then sorted index, scenario_tree.py:39)
+ *   nonant_depth[nn], nonant_off[nn]    host, tree depth of k's node / offset in it
+ *   depth                               number of non-leaf nodes per scenario
+ *   num_nodes, nlen_max                 size of the node-indexed x̄ buffer
+ *                                       (num_nodes * nlen_max entries per half) */
+int phgpu_create(phgpu_handle* h, int device, int64_t S, int32_t n, int32_t m, int32_t nnz,
+                 const int32_t* row_ptr, const int32_t* col_idx, int32_t nn,
+                 const int32_t* nonant_col, const int32_t* nonant_depth,
+                 const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
+                 int32_t nlen_max);
+
+/* Upload per-scenario data (device pointers, scenario-fastest):
+ *   A_val[nnz*S], c/lb/ub/q[n*S] (q may be NULL = 0), rl/ru[m*S] (+-inf allowed),
+ *   obj_const[S] (may be NULL), prob[S], node_of[depth*S] (int32 global node id),
+ *   prob_coeff[depth*S] (pi_s / pi_node, spbase.py:384-391).
+ * Computes the diagonal (Ruiz + Pock-Chambolle) scaling and ||A_scaled||_2 per
+ * scenario; replaces the per-scenario Pyomo model construction of
+ * SPBase._create_scenarios (spbase.py:255-291). */
+int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
+                        const double* lb, const double* ub, const double* rl,
+                        const double* ru, const double* q, const double* obj_const,
+                        const double* prob, const int32_t* node_of,
+                        const double* prob_coeff, void* stream);
+
+/* Bind the PH objective terms for the next solves (phbase.py:585-699):
+ *   objective = f(x) + W_on * sum_k W[k,s] x_k + prox_on * sum_k rho[k,s]/2 (x_k - xbar[k,s])^2
+ * W, rho, xbar: device [nn*S]; they are read at solve time (not copied). */
+int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
+                       const double* xbar, int W_on, int prox_on);
+
+/* Solve all local scenarios (SPOpt.solve_loop, spopt.py:226-307).
+ *   warm_start   1: start from the previous solution (x, y) of this handle
+ *   x[n*S]       device out: primal solution (all columns)
+ *   y[m*S]       device out (may be NULL): row duals (positive = lower bound active)
+ *   obj[S]       device out: augmented objective incl. PH terms (what
+ *                Eobjective sums, spopt.py:332-333)
+ *   bound[S]     device out: Lagrangian dual bound (results.Problem[0].Lower_bound,
+ *                spopt.py:201-206)
+ *   status[S]    device out: PHGPU_* code
+ *   iters[S]     device out (may be NULL): PDHG iterations used                 */
+int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
+                double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
+                void* stream);
+
+/* Local x̄ partial sums (phbase.py:54-79): node_buf[2*num_nodes*nlen_max] gets
+ *   [g*nlen_max + o]                        sum_s prob_coeff * x
+ *   [num_nodes*nlen_max + g*nlen_max + o]   sum_s prob_coeff * x^2
+ * over the local scenarios whose depth-d node is g.  node_buf is overwritten. */
+int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream);
+
+/* After the cross-rank sum of node_buf: scatter x̄ to every local scenario
+ * (phbase.py:90-103), W += rho (x - x̄) if update_W (phbase.py:293-318), and
+ * conv_local[0] = sum_{s,k} |x - x̄| / (S * nn)  (phbase.py:330-339; the caller
+ * sums over ranks and divides by n_proc, phbase.py:341-343).
+ *   xbar, W: device [nn*S] (xbar written, W updated in place). */
+int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, double* xbar,
+                    double* W, const double* rho, int update_W, double* conv_local,
+                    void* stream);
+
+/* Local probability-weighted sums (spopt.py:310-439) into out[4]:
+ *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
+ *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s: status==OPTIMAL} prob_s */
+int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
+                       const int32_t* status, double* out, void* stream);
+
+/* Free the workspace and the handle. */
+int phgpu_destroy(phgpu_handle h);
+
+/* Copy the calling thread's last error message (NUL-terminated) into buf. */
+int phgpu_last_error(char* buf, size_t len);
+
+/* Workspace bytes held by the handle (diagnostics / memory planning). */
+int64_t phgpu_workspace_bytes(phgpu_handle h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHGPU_H */

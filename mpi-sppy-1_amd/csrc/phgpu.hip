@@ -1,0 +1,867 @@
+// phgpu.hip -- MI355X (gfx950) kernels + C-ABI for the batched PH hot path.
+//
+// Design: every local scenario is one LP/QP that shares the CSR
+// pattern of the rank; per-scenario arrays are stored scenario-fastest ([k][S]) so
+// that the 64 lanes of a wavefront process 64 scenarios and every load/store of a
+// pattern position is one coalesced 512-byte access, while the pattern itself
+// (row_ptr, col_idx, col_ptr, row_idx, perm) is wave-uniform and goes through the
+// scalar cache.  One lane runs its scenario's whole restarted-Halpern PDHG solve in a
+// single launch (no grid-wide synchronisation: scenarios are independent), with its
+// own primal weight, restart state and KKT termination test.
+//
+// Reference behaviour replaced (mpi-sppy, /root/reference):
+//   SPOpt.solve_loop / solve_one        spopt.py:226-307 / 85-223
+//   PH objective terms                  phbase.py:617-699
+//   _Compute_Xbar / Update_W / conv     phbase.py:27-107, 293-343
+//   Ebound / Eobjective / E1 / feas     spopt.py:310-439
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+#include <new>
+
+#include "phgpu.h"
+
+#define WAVE 64
+#define BLOCK 64
+
+// ------------------------------------------------------------------ errors
+static thread_local char g_err[512] = {0};
+
+static int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIPCHK(call)                                                                 \
+    do {                                                                             \
+        hipError_t e_ = (call);                                                      \
+        if (e_ != hipSuccess)                                                        \
+            return set_err(-2, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                      \
+    } while (0)
+
+// ------------------------------------------------------------------ state
+struct phgpu_state {
+    int device;
+    int64_t S;
+    int n, m, nnz, nn, depth, num_nodes, nlen_max;
+    // shared pattern
+    int32_t *row_ptr, *col_idx, *col_ptr, *row_idx, *perm, *row_of;
+    int32_t *nonant_col, *nonant_depth, *nonant_off, *nonant_slot;
+    // per-scenario problem data (library copies)
+    double *A, *c, *lb, *ub, *rl, *ru, *q, *objc, *prob, *pcoef;
+    int32_t* node_of;
+    // scaling
+    double *Ah_csr, *Ah_csc, *Dr, *Dc, *normA;
+    double *lbh, *ubh, *rlh, *ruh;
+    // per-solve effective objective (scaled) + iterates (scaled)
+    double *ch, *qh;
+    double *x, *x0, *xe, *xt, *aty, *aty0, *y, *y0, *yt;
+    double* omega;
+    // reductions
+    double* part;       // [nwaves * max(2*nn, 4)]
+    int32_t* part_node; // [nwaves * nn]
+    int64_t nwaves;
+    int64_t ws_bytes;
+    // PH state (caller-owned)
+    const double *W, *rho, *xbar;
+    int W_on, prox_on;
+    int have_solution;
+};
+
+#define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
+
+// ------------------------------------------------------------------ device helpers
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, WAVE);
+    return v;
+}
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) {
+    return fmin(fmax(v, lo), hi);
+}
+
+// y-part of the PDHG dual step for a ranged row rl <= a'x <= ru:
+// maximise -y*ax + (rl y+ - ru y-) - (y - yk)^2/(2 sig)
+__device__ __forceinline__ double dual_prox(double v, double sig, double rlh, double ruh) {
+    double a = v + sig * rlh;
+    double b = v + sig * ruh;
+    return a > 0.0 ? a : (b < 0.0 ? b : 0.0);
+}
+
+// contribution of row i to the Lagrangian dual objective: min_{s in [rl,ru]} y s,
+// projected (an infinite side with the wrong-sign multiplier contributes 0)
+__device__ __forceinline__ double row_dual_term(double y, double rl, double ru) {
+    if (y > 0.0) return isfinite(rl) ? rl * y : 0.0;
+    if (y < 0.0) return isfinite(ru) ? ru * y : 0.0;
+    return 0.0;
+}
+
+// min over x in [lb,ub] of r x + q/2 x^2 (projected for infinite sides when q == 0)
+__device__ __forceinline__ double col_dual_term(double r, double qq, double lb, double ub) {
+    if (qq > 0.0) {
+        double xm = clampd(-r / qq, lb, ub);
+        return r * xm + 0.5 * qq * xm * xm;
+    }
+    if (r > 0.0) return isfinite(lb) ? r * lb : 0.0;
+    if (r < 0.0) return isfinite(ub) ? r * ub : 0.0;
+    return 0.0;
+}
+
+// ------------------------------------------------------------------ setup kernel
+// Per scenario: copy A, Ruiz (iters) + Pock-Chambolle(alpha=1) scaling, scaled
+// bounds, CSC copy of the scaled values and ||A_scaled||_2 by power iteration.
+__global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters, int power_iters) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int n = st.n, m = st.m, nnz = st.nnz;
+    double* Ah = st.Ah_csr;
+    for (int k = 0; k < nnz; ++k) Ah[IX(k)] = st.A[IX(k)];
+    for (int i = 0; i < m; ++i) st.Dr[IX(i)] = 1.0;
+    for (int j = 0; j < n; ++j) st.Dc[IX(j)] = 1.0;
+    // temporaries: row factors in yt, column factors in xt
+    for (int pass = 0; pass <= ruiz_iters; ++pass) {
+        const bool pc = (pass == ruiz_iters);  // last pass: Pock-Chambolle alpha = 1
+        for (int i = 0; i < m; ++i) {
+            double a = 0.0;
+            for (int k = st.row_ptr[i]; k < st.row_ptr[i + 1]; ++k) {
+                double v = fabs(Ah[IX(k)]);
+                a = pc ? a + v : fmax(a, v);
+            }
+            st.yt[IX(i)] = a > 0.0 ? 1.0 / sqrt(a) : 1.0;
+        }
+        for (int j = 0; j < n; ++j) {
+            double a = 0.0;
+            for (int kc = st.col_ptr[j]; kc < st.col_ptr[j + 1]; ++kc) {
+                double v = fabs(Ah[IX(st.perm[kc])]);
+                a = pc ? a + v : fmax(a, v);
+            }
+            st.xt[IX(j)] = a > 0.0 ? 1.0 / sqrt(a) : 1.0;
+        }
+        for (int i = 0; i < m; ++i) {
+            const double ri = st.yt[IX(i)];
+            st.Dr[IX(i)] *= ri;
+            for (int k = st.row_ptr[i]; k < st.row_ptr[i + 1]; ++k)
+                Ah[IX(k)] *= ri * st.xt[IX(st.col_idx[k])];
+        }
+        for (int j = 0; j < n; ++j) st.Dc[IX(j)] *= st.xt[IX(j)];
+    }
+    for (int kc = 0; kc < nnz; ++kc) st.Ah_csc[IX(kc)] = Ah[IX(st.perm[kc])];
+    for (int j = 0; j < n; ++j) {
+        const double d = st.Dc[IX(j)];
+        st.lbh[IX(j)] = st.lb[IX(j)] / d;
+        st.ubh[IX(j)] = st.ub[IX(j)] / d;
+        st.x[IX(j)] = 0.0;
+    }
+    for (int i = 0; i < m; ++i) {
+        const double d = st.Dr[IX(i)];
+        st.rlh[IX(i)] = st.rl[IX(i)] * d;
+        st.ruh[IX(i)] = st.ru[IX(i)] * d;
+        st.y[IX(i)] = 0.0;
+    }
+    // power iteration on A^T A (v in xe, A v in yt, A^T A v in xt)
+    for (int j = 0; j < n; ++j) st.xe[IX(j)] = 1.0;
+    double lam = 0.0;
+    for (int it = 0; it < power_iters; ++it) {
+        for (int i = 0; i < m; ++i) {
+            double a = 0.0;
+            for (int k = st.row_ptr[i]; k < st.row_ptr[i + 1]; ++k)
+                a += Ah[IX(k)] * st.xe[IX(st.col_idx[k])];
+            st.yt[IX(i)] = a;
+        }
+        double nv = 0.0;
+        for (int j = 0; j < n; ++j) {
+            double a = 0.0;
+            for (int kc = st.col_ptr[j]; kc < st.col_ptr[j + 1]; ++kc)
+                a += st.Ah_csc[IX(kc)] * st.yt[IX(st.row_idx[kc])];
+            st.xt[IX(j)] = a;
+            nv += a * a;
+        }
+        nv = sqrt(nv);
+        lam = nv;  // ||A^T A v|| with ||v|| = 1 (after the first pass)
+        const double inv = nv > 0.0 ? 1.0 / nv : 0.0;
+        for (int j = 0; j < n; ++j) st.xe[IX(j)] = st.xt[IX(j)] * inv;
+    }
+    st.normA[s] = lam > 0.0 ? sqrt(lam) : 1.0;
+    st.omega[s] = 1.0;
+}
+
+// ------------------------------------------------------------------ solve kernel
+struct solve_params {
+    double eps_rel, eps_abs, gamma, bsuff, bnec, eta_frac, omega0;
+    int max_iter, check_every, warm, keep_omega;
+};
+
+__global__ void __launch_bounds__(BLOCK)
+k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __restrict__ yout,
+        double* __restrict__ obj, double* __restrict__ bound, int32_t* __restrict__ status,
+        int32_t* __restrict__ iters) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int n = st.n, m = st.m;
+    const int32_t* __restrict__ row_ptr = st.row_ptr;
+    const int32_t* __restrict__ col_idx = st.col_idx;
+    const int32_t* __restrict__ col_ptr = st.col_ptr;
+    const int32_t* __restrict__ row_idx = st.row_idx;
+    const double* __restrict__ Ahr = st.Ah_csr;
+    const double* __restrict__ Ahc = st.Ah_csc;
+    double* __restrict__ x = st.x;
+    double* __restrict__ x0 = st.x0;
+    double* __restrict__ xe = st.xe;
+    double* __restrict__ xt = st.xt;
+    double* __restrict__ aty = st.aty;
+    double* __restrict__ aty0 = st.aty0;
+    double* __restrict__ y = st.y;
+    double* __restrict__ y0 = st.y0;
+    double* __restrict__ yt = st.yt;
+    const double* __restrict__ ch = st.ch;
+    const double* __restrict__ qh = st.qh;
+
+    // ---- effective objective of this solve (phbase.py:617-699), scaled
+    double cnorm2 = 0.0, const_term = st.objc ? st.objc[s] : 0.0;
+    for (int j = 0; j < n; ++j) {
+        double cj = st.c[IX(j)];
+        double qj = st.q ? st.q[IX(j)] : 0.0;
+        const int k = st.nonant_slot[j];
+        if (k >= 0) {
+            if (st.W_on) cj += st.W[IX(k)];
+            if (st.prox_on) {
+                const double r = st.rho[IX(k)], xb = st.xbar[IX(k)];
+                cj -= r * xb;
+                qj += r;
+                const_term += 0.5 * r * xb * xb;
+            }
+        }
+        const double d = st.Dc[IX(j)];
+        st.ch[IX(j)] = d * cj;
+        st.qh[IX(j)] = d * d * qj;
+        cnorm2 += cj * cj;
+    }
+    double bnorm2 = 0.0;
+    for (int i = 0; i < m; ++i) {
+        const double a = st.rl[IX(i)], b = st.ru[IX(i)];
+        if (isfinite(a)) bnorm2 += a * a;
+        if (isfinite(b) && b != a) bnorm2 += b * b;
+    }
+    const double cnorm = sqrt(cnorm2), bnorm = sqrt(bnorm2);
+
+    // ---- start point
+    for (int j = 0; j < n; ++j) {
+        double v = P.warm ? x[IX(j)] : 0.0;
+        v = clampd(v, st.lbh[IX(j)], st.ubh[IX(j)]);
+        x[IX(j)] = v;
+        x0[IX(j)] = v;
+    }
+    for (int i = 0; i < m; ++i) {
+        const double v = P.warm ? y[IX(i)] : 0.0;
+        y[IX(i)] = v;
+        y0[IX(i)] = v;
+    }
+    for (int j = 0; j < n; ++j) {
+        double a = 0.0;
+        for (int kc = col_ptr[j]; kc < col_ptr[j + 1]; ++kc) a += Ahc[IX(kc)] * y[IX(row_idx[kc])];
+        aty[IX(j)] = a;
+        aty0[IX(j)] = a;
+    }
+    double omega = st.omega[s];
+    if (!(P.keep_omega && P.warm) && P.omega0 > 0.0) omega = P.omega0;
+    const double eta = P.eta_frac / st.normA[s];
+    const double g = P.gamma;
+
+    double r0 = -1.0, rlast = INFINITY;
+    double pobj = 0.0, dobj = 0.0;
+    int hk = 0;  // Halpern counter since the last restart
+    int it = 0;
+    int stat = PHGPU_ITER_LIMIT;
+    bool final_is_t = false;  // true: solution is T(z) (in xt/yt/xe)
+    for (; it < P.max_iter; ++it) {
+        const double tau = eta / omega, sig = eta * omega;
+        const bool check = (it % P.check_every) == 0;
+        const double a1 = (hk + 1.0) / (hk + 2.0), a0 = 1.0 / (hk + 2.0);
+        double dx2 = 0.0, dy2 = 0.0;
+        // --- primal step: xt = prox(x - tau (c - A^T y)); xe = 2 xt - x
+        for (int j = 0; j < n; ++j) {
+            const double xj = x[IX(j)];
+            const double xtj = clampd((xj - tau * (ch[IX(j)] - aty[IX(j)])) / (1.0 + tau * qh[IX(j)]),
+                                      st.lbh[IX(j)], st.ubh[IX(j)]);
+            xe[IX(j)] = 2.0 * xtj - xj;
+            const double d = xj - xtj;
+            dx2 += d * d;
+            if (check) xt[IX(j)] = xtj;
+            else x[IX(j)] = a1 * ((1.0 + g) * xtj - g * xj) + a0 * x0[IX(j)];
+        }
+        // --- dual step: yt = prox(y - sig A xe)
+        for (int i = 0; i < m; ++i) {
+            double ax = 0.0;
+            for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) ax += Ahr[IX(k)] * xe[IX(col_idx[k])];
+            const double yi = y[IX(i)];
+            const double yti = dual_prox(yi - sig * ax, sig, st.rlh[IX(i)], st.ruh[IX(i)]);
+            yt[IX(i)] = yti;
+            const double d = yi - yti;
+            dy2 += d * d;
+            if (!check) y[IX(i)] = a1 * ((1.0 + g) * yti - g * yi) + a0 * y0[IX(i)];
+        }
+        // --- A^T yt (Halpern-combined in place, or kept in xe at checks)
+        for (int j = 0; j < n; ++j) {
+            double a = 0.0;
+            for (int kc = col_ptr[j]; kc < col_ptr[j + 1]; ++kc) a += Ahc[IX(kc)] * yt[IX(row_idx[kc])];
+            if (check) xe[IX(j)] = a;
+            else aty[IX(j)] = a1 * ((1.0 + g) * a - g * aty[IX(j)]) + a0 * aty0[IX(j)];
+        }
+        const double r = sqrt(omega * dx2 + dy2 / omega);
+        if (r0 < 0.0) r0 = r;
+        if (!check) {
+            ++hk;
+            continue;
+        }
+        // ---- KKT test on T(z) = (xt, yt), original space
+        double pres2 = 0.0, dres2 = 0.0;
+        pobj = const_term;
+        dobj = const_term;
+        for (int i = 0; i < m; ++i) {
+            double ax = 0.0;
+            for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) ax += Ahr[IX(k)] * xt[IX(col_idx[k])];
+            const double dr = st.Dr[IX(i)];
+            ax /= dr;
+            const double rl = st.rl[IX(i)], ru = st.ru[IX(i)];
+            const double v = ax - clampd(ax, rl, ru);
+            pres2 += v * v;
+            dobj += row_dual_term(yt[IX(i)] * dr, rl, ru);
+        }
+        for (int j = 0; j < n; ++j) {
+            const double d = st.Dc[IX(j)];
+            const double xo = d * xt[IX(j)];
+            const double ce = ch[IX(j)] / d, qe = qh[IX(j)] / (d * d);
+            const double at = xe[IX(j)] / d;
+            const double lbj = st.lb[IX(j)], ubj = st.ub[IX(j)];
+            const double rc = ce + qe * xo - at;
+            double lam;
+            if (isfinite(lbj) && isfinite(ubj)) lam = rc;
+            else if (isfinite(lbj)) lam = fmax(rc, 0.0);
+            else if (isfinite(ubj)) lam = fmin(rc, 0.0);
+            else lam = 0.0;
+            const double dr = rc - lam;
+            dres2 += dr * dr;
+            pobj += ce * xo + 0.5 * qe * xo * xo;
+            dobj += col_dual_term(ce - at, qe, lbj, ubj);
+        }
+        const bool conv = sqrt(pres2) <= P.eps_abs + P.eps_rel * (1.0 + bnorm) &&
+                          sqrt(dres2) <= P.eps_abs + P.eps_rel * (1.0 + cnorm) &&
+                          fabs(pobj - dobj) <= P.eps_abs + P.eps_rel * (1.0 + fabs(pobj) + fabs(dobj));
+        if (conv) {
+            stat = PHGPU_OPTIMAL;
+            final_is_t = true;
+            break;
+        }
+        // ---- restart test (cuPDLP+-style: sufficient / necessary-without-progress)
+        const bool restart = (r <= P.bsuff * r0) || (r <= P.bnec * r0 && r > rlast);
+        rlast = r;
+        if (restart) {
+            double ddx = 0.0, ddy = 0.0;
+            for (int j = 0; j < n; ++j) {
+                const double v = xt[IX(j)];
+                const double d = v - x0[IX(j)];
+                ddx += d * d;
+                x[IX(j)] = v;
+                x0[IX(j)] = v;
+                aty[IX(j)] = xe[IX(j)];
+                aty0[IX(j)] = xe[IX(j)];
+            }
+            for (int i = 0; i < m; ++i) {
+                const double v = yt[IX(i)];
+                const double d = v - y0[IX(i)];
+                ddy += d * d;
+                y[IX(i)] = v;
+                y0[IX(i)] = v;
+            }
+            ddx = sqrt(ddx);
+            ddy = sqrt(ddy);
+            if (ddx > 1e-10 && ddy > 1e-10) omega = exp(0.5 * log(ddy / ddx) + 0.5 * log(omega));
+            hk = 0;
+            r0 = -1.0;
+            rlast = INFINITY;
+        } else {
+            for (int j = 0; j < n; ++j) {
+                x[IX(j)] = a1 * ((1.0 + g) * xt[IX(j)] - g * x[IX(j)]) + a0 * x0[IX(j)];
+                aty[IX(j)] = a1 * ((1.0 + g) * xe[IX(j)] - g * aty[IX(j)]) + a0 * aty0[IX(j)];
+            }
+            for (int i = 0; i < m; ++i)
+                y[IX(i)] = a1 * ((1.0 + g) * yt[IX(i)] - g * y[IX(i)]) + a0 * y0[IX(i)];
+            ++hk;
+        }
+    }
+    // ---- write back: converged -> T(z); iteration limit -> current z
+    if (final_is_t) {
+        for (int j = 0; j < n; ++j) x[IX(j)] = xt[IX(j)];
+        for (int i = 0; i < m; ++i) y[IX(i)] = yt[IX(i)];
+    } else {
+        // objective / bound at the current iterate
+        pobj = const_term;
+        dobj = const_term;
+        for (int i = 0; i < m; ++i) dobj += row_dual_term(y[IX(i)] * st.Dr[IX(i)], st.rl[IX(i)], st.ru[IX(i)]);
+        for (int j = 0; j < n; ++j) {
+            const double d = st.Dc[IX(j)];
+            const double xo = d * x[IX(j)];
+            const double ce = ch[IX(j)] / d, qe = qh[IX(j)] / (d * d);
+            pobj += ce * xo + 0.5 * qe * xo * xo;
+            dobj += col_dual_term(ce - aty[IX(j)] / d, qe, st.lb[IX(j)], st.ub[IX(j)]);
+        }
+    }
+    for (int j = 0; j < n; ++j) xout[IX(j)] = st.Dc[IX(j)] * x[IX(j)];
+    if (yout)
+        for (int i = 0; i < m; ++i) yout[IX(i)] = st.Dr[IX(i)] * y[IX(i)];
+    st.omega[s] = omega;
+    obj[s] = pobj;
+    bound[s] = dobj;
+    status[s] = stat;
+    if (iters) iters[s] = final_is_t ? it : P.max_iter;
+}
+
+// ------------------------------------------------------------------ PH reductions
+// phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
+// each nonant; a wave whose scenarios share one node at that depth writes one
+// partial (deterministic); a mixed wave adds per lane with fp64 atomics.
+__global__ void __launch_bounds__(BLOCK)
+k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t wave = s / WAVE;
+    const bool act = s < S;
+    const int half = st.num_nodes * st.nlen_max;
+    for (int k = 0; k < st.nn; ++k) {
+        const int d = st.nonant_depth[k];
+        const int gnode = act ? st.node_of[IX(d)] : -1;
+        const double w = act ? st.pcoef[IX(d)] : 0.0;
+        const double v = act ? x[IX(st.nonant_col[k])] : 0.0;
+        const int g0 = __shfl(gnode, 0, WAVE);
+        const bool uniform = !__any(act && gnode != g0);
+        if (uniform) {
+            const double a = wave_sum(w * v);
+            const double b = wave_sum(w * v * v);
+            if ((threadIdx.x & (WAVE - 1)) == 0) {
+                st.part[(wave * st.nn + k) * 2 + 0] = a;
+                st.part[(wave * st.nn + k) * 2 + 1] = b;
+                st.part_node[wave * st.nn + k] = g0;
+            }
+        } else {
+            if (act) {
+                const int o = gnode * st.nlen_max + st.nonant_off[k];
+                atomicAdd(&node_buf[o], w * v);
+                atomicAdd(&node_buf[half + o], w * v * v);
+            }
+            if ((threadIdx.x & (WAVE - 1)) == 0) st.part_node[wave * st.nn + k] = -1;
+        }
+    }
+}
+
+// One thread per nonant: ordered run-sum over the waves' partials.
+__global__ void k_xbar_final(phgpu_state st, double* __restrict__ node_buf) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= st.nn) return;
+    const int half = st.num_nodes * st.nlen_max;
+    const int off = st.nonant_off[k];
+    int cur = -1;
+    double a = 0.0, b = 0.0;
+    for (int64_t w = 0; w < st.nwaves; ++w) {
+        const int gnode = st.part_node[w * st.nn + k];
+        if (gnode < 0) continue;
+        if (gnode != cur) {
+            if (cur >= 0) {
+                node_buf[cur * st.nlen_max + off] += a;
+                node_buf[half + cur * st.nlen_max + off] += b;
+            }
+            cur = gnode;
+            a = 0.0;
+            b = 0.0;
+        }
+        a += st.part[(w * st.nn + k) * 2 + 0];
+        b += st.part[(w * st.nn + k) * 2 + 1];
+    }
+    if (cur >= 0) {
+        node_buf[cur * st.nlen_max + off] += a;
+        node_buf[half + cur * st.nlen_max + off] += b;
+    }
+}
+
+// phbase.py:90-103 (scatter x̄), 293-318 (W update), 330-339 (local |x - x̄| sum).
+__global__ void __launch_bounds__(BLOCK)
+k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restrict__ node_buf,
+            double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
+            int update_W) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0.0;
+    if (s < S) {
+        for (int k = 0; k < st.nn; ++k) {
+            const int d = st.nonant_depth[k];
+            const int gnode = st.node_of[IX(d)];
+            const double xb = node_buf[gnode * st.nlen_max + st.nonant_off[k]];
+            const double xv = x[IX(st.nonant_col[k])];
+            xbar[IX(k)] = xb;
+            if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
+            acc += fabs(xv - xb);
+        }
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & (WAVE - 1)) == 0) st.part[s / WAVE] = acc;
+}
+
+// spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible.
+__global__ void __launch_bounds__(BLOCK)
+k_expect_partial(phgpu_state st, const double* __restrict__ obj, const double* __restrict__ bound,
+                 const int32_t* __restrict__ status) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if (s < S) {
+        const double p = st.prob[s];
+        v[0] = p * obj[s];
+        v[1] = p * bound[s];
+        v[2] = p;
+        v[3] = status[s] == PHGPU_OPTIMAL ? p : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double a = wave_sum(v[t]);
+        if ((threadIdx.x & (WAVE - 1)) == 0) st.part[(s / WAVE) * 4 + t] = a;
+    }
+}
+
+// Deterministic ordered sum of K interleaved per-wave partials: out[k] = sum_w part[w*K+k].
+__global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__ part, int64_t nw, int K,
+                                                     double scale, double* __restrict__ out) {
+    __shared__ double sh[256];
+    const int k = blockIdx.x;
+    double a = 0.0;
+    for (int64_t w = threadIdx.x; w < nw; w += 256) a += part[w * K + k];
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[k] = sh[0] * scale;
+}
+
+// ------------------------------------------------------------------ C-ABI
+template <typename T>
+static int dalloc(phgpu_state* h, T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return set_err(-3, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
+    h->ws_bytes += (int64_t)(count * sizeof(T));
+    return 0;
+}
+
+#define ALLOC(ptr, cnt)                         \
+    do {                                        \
+        int rc_ = dalloc(h, &(ptr), (size_t)(cnt)); \
+        if (rc_) { phgpu_destroy(h); return rc_; } \
+    } while (0)
+
+extern "C" int phgpu_default_options(phgpu_options* o) {
+    if (!o) return set_err(-1, "null options");
+    o->eps_rel = 1e-10;
+    o->eps_abs = 1e-12;
+    o->max_iter = 100000;
+    o->check_every = 64;
+    o->gamma = 1.0;
+    o->beta_sufficient = 0.2;
+    o->beta_necessary = 0.8;
+    o->eta_frac = 0.998;
+    o->omega0 = 1.0;
+    o->keep_omega = 1;
+    o->reserved = 0;
+    return 0;
+}
+
+extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n, int32_t m,
+                            int32_t nnz, const int32_t* row_ptr, const int32_t* col_idx,
+                            int32_t nn, const int32_t* nonant_col, const int32_t* nonant_depth,
+                            const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
+                            int32_t nlen_max) {
+    if (!out) return set_err(-1, "null handle pointer");
+    *out = nullptr;
+    if (S <= 0 || n <= 0 || m < 0 || nnz < 0 || nn < 0 || depth < 1 || num_nodes < 1 || nlen_max < 0)
+        return set_err(-1, "bad sizes S=%lld n=%d m=%d nnz=%d nn=%d depth=%d nodes=%d",
+                       (long long)S, n, m, nnz, nn, depth, num_nodes);
+    if (!row_ptr || (nnz > 0 && !col_idx) || (nn > 0 && (!nonant_col || !nonant_depth || !nonant_off)))
+        return set_err(-1, "null pattern pointer");
+    // host-side validation of the shared pattern
+    if (row_ptr[0] != 0 || row_ptr[m] != nnz) return set_err(-1, "row_ptr must start at 0 and end at nnz");
+    for (int i = 0; i < m; ++i)
+        if (row_ptr[i + 1] < row_ptr[i]) return set_err(-1, "row_ptr not monotone at row %d", i);
+    for (int k = 0; k < nnz; ++k)
+        if (col_idx[k] < 0 || col_idx[k] >= n) return set_err(-1, "col_idx[%d]=%d out of range", k, col_idx[k]);
+    int32_t* slot = new int32_t[n];
+    for (int j = 0; j < n; ++j) slot[j] = -1;
+    for (int k = 0; k < nn; ++k) {
+        if (nonant_col[k] < 0 || nonant_col[k] >= n || slot[nonant_col[k]] >= 0 ||
+            nonant_depth[k] < 0 || nonant_depth[k] >= depth || nonant_off[k] < 0 ||
+            nonant_off[k] >= nlen_max) {
+            delete[] slot;
+            return set_err(-1, "bad nonant map at %d", k);
+        }
+        slot[nonant_col[k]] = k;
+    }
+    HIPCHK(hipSetDevice(device));
+    phgpu_state* h = new (std::nothrow) phgpu_state();
+    if (!h) {
+        delete[] slot;
+        return set_err(-3, "out of host memory");
+    }
+    memset(h, 0, sizeof(*h));
+    h->device = device;
+    h->S = S;
+    h->n = n;
+    h->m = m;
+    h->nnz = nnz;
+    h->nn = nn;
+    h->depth = depth;
+    h->num_nodes = num_nodes;
+    h->nlen_max = nlen_max;
+    h->nwaves = (S + WAVE - 1) / WAVE;
+    // transposed pattern (host)
+    int32_t* cptr = new int32_t[n + 1]();
+    int32_t* ridx = new int32_t[nnz > 0 ? nnz : 1];
+    int32_t* perm = new int32_t[nnz > 0 ? nnz : 1];
+    int32_t* rowof = new int32_t[nnz > 0 ? nnz : 1];
+    for (int k = 0; k < nnz; ++k) cptr[col_idx[k] + 1]++;
+    for (int j = 0; j < n; ++j) cptr[j + 1] += cptr[j];
+    {
+        int32_t* fill = new int32_t[n];
+        for (int j = 0; j < n; ++j) fill[j] = cptr[j];
+        for (int i = 0; i < m; ++i)
+            for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+                const int p = fill[col_idx[k]]++;
+                ridx[p] = i;
+                perm[p] = k;
+                rowof[k] = i;
+            }
+        delete[] fill;
+    }
+    const size_t Sz = (size_t)S;
+    int rc = 0;
+    ALLOC(h->row_ptr, m + 1);
+    ALLOC(h->col_idx, nnz);
+    ALLOC(h->col_ptr, n + 1);
+    ALLOC(h->row_idx, nnz);
+    ALLOC(h->perm, nnz);
+    ALLOC(h->row_of, nnz);
+    ALLOC(h->nonant_col, nn);
+    ALLOC(h->nonant_depth, nn);
+    ALLOC(h->nonant_off, nn);
+    ALLOC(h->nonant_slot, n);
+    ALLOC(h->A, (size_t)nnz * Sz);
+    ALLOC(h->c, (size_t)n * Sz);
+    ALLOC(h->lb, (size_t)n * Sz);
+    ALLOC(h->ub, (size_t)n * Sz);
+    ALLOC(h->q, (size_t)n * Sz);
+    ALLOC(h->rl, (size_t)m * Sz);
+    ALLOC(h->ru, (size_t)m * Sz);
+    ALLOC(h->objc, Sz);
+    ALLOC(h->prob, Sz);
+    ALLOC(h->pcoef, (size_t)depth * Sz);
+    ALLOC(h->node_of, (size_t)depth * Sz);
+    ALLOC(h->Ah_csr, (size_t)nnz * Sz);
+    ALLOC(h->Ah_csc, (size_t)nnz * Sz);
+    ALLOC(h->Dr, (size_t)m * Sz);
+    ALLOC(h->Dc, (size_t)n * Sz);
+    ALLOC(h->normA, Sz);
+    ALLOC(h->lbh, (size_t)n * Sz);
+    ALLOC(h->ubh, (size_t)n * Sz);
+    ALLOC(h->rlh, (size_t)m * Sz);
+    ALLOC(h->ruh, (size_t)m * Sz);
+    ALLOC(h->ch, (size_t)n * Sz);
+    ALLOC(h->qh, (size_t)n * Sz);
+    ALLOC(h->x, (size_t)n * Sz);
+    ALLOC(h->x0, (size_t)n * Sz);
+    ALLOC(h->xe, (size_t)n * Sz);
+    ALLOC(h->xt, (size_t)n * Sz);
+    ALLOC(h->aty, (size_t)n * Sz);
+    ALLOC(h->aty0, (size_t)n * Sz);
+    ALLOC(h->y, (size_t)m * Sz);
+    ALLOC(h->y0, (size_t)m * Sz);
+    ALLOC(h->yt, (size_t)m * Sz);
+    ALLOC(h->omega, Sz);
+    {
+        size_t K = (size_t)(2 * nn > 4 ? 2 * nn : 4);
+        ALLOC(h->part, (size_t)h->nwaves * K);
+        ALLOC(h->part_node, (size_t)h->nwaves * (nn > 0 ? nn : 1));
+    }
+    (void)rc;
+    hipError_t e = hipSuccess;
+    e = hipMemcpy(h->row_ptr, row_ptr, (m + 1) * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(h->col_idx, col_idx, nnz * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->col_ptr, cptr, (n + 1) * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(h->row_idx, ridx, nnz * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(h->perm, perm, nnz * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(h->row_of, rowof, nnz * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nn) e = hipMemcpy(h->nonant_col, nonant_col, nn * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nn) e = hipMemcpy(h->nonant_depth, nonant_depth, nn * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nn) e = hipMemcpy(h->nonant_off, nonant_off, nn * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->nonant_slot, slot, n * sizeof(int32_t), hipMemcpyHostToDevice);
+    delete[] cptr;
+    delete[] ridx;
+    delete[] perm;
+    delete[] rowof;
+    delete[] slot;
+    if (e != hipSuccess) {
+        phgpu_destroy(h);
+        return set_err(-2, "pattern upload failed: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return 0;
+}
+
+static inline dim3 grid_for(int64_t S) { return dim3((unsigned)((S + BLOCK - 1) / BLOCK)); }
+
+extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
+                                   const double* lb, const double* ub, const double* rl,
+                                   const double* ru, const double* q, const double* obj_const,
+                                   const double* prob, const int32_t* node_of,
+                                   const double* prob_coeff, void* stream) {
+    if (!h) return set_err(-1, "null handle");
+    if ((h->nnz && !A_val) || !c || !lb || !ub || (h->m && (!rl || !ru)) || !prob || !node_of || !prob_coeff)
+        return set_err(-1, "null scenario array");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t Sz = (size_t)h->S;
+    auto cp = [&](double* dst, const double* src, size_t cnt) -> hipError_t {
+        if (cnt == 0) return hipSuccess;
+        return hipMemcpyAsync(dst, src, cnt * sizeof(double), hipMemcpyDeviceToDevice, st);
+    };
+    HIPCHK(cp(h->A, A_val, (size_t)h->nnz * Sz));
+    HIPCHK(cp(h->c, c, (size_t)h->n * Sz));
+    HIPCHK(cp(h->lb, lb, (size_t)h->n * Sz));
+    HIPCHK(cp(h->ub, ub, (size_t)h->n * Sz));
+    HIPCHK(cp(h->rl, rl, (size_t)h->m * Sz));
+    HIPCHK(cp(h->ru, ru, (size_t)h->m * Sz));
+    if (q) HIPCHK(cp(h->q, q, (size_t)h->n * Sz));
+    else HIPCHK(hipMemsetAsync(h->q, 0, (size_t)h->n * Sz * sizeof(double), st));
+    if (obj_const) HIPCHK(cp(h->objc, obj_const, Sz));
+    else HIPCHK(hipMemsetAsync(h->objc, 0, Sz * sizeof(double), st));
+    HIPCHK(cp(h->prob, prob, Sz));
+    HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
+    HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_setup, grid_for(h->S), dim3(BLOCK), 0, st, *h, 10, 40);
+    HIPCHK(hipGetLastError());
+    h->have_solution = 0;
+    return 0;
+}
+
+extern "C" int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
+                                  const double* xbar, int W_on, int prox_on) {
+    if (!h) return set_err(-1, "null handle");
+    if (h->nn > 0 && ((W_on && !W) || (prox_on && (!rho || !xbar))))
+        return set_err(-1, "W / rho / xbar pointer missing for the requested terms");
+    h->W = W;
+    h->rho = rho;
+    h->xbar = xbar;
+    h->W_on = W_on ? 1 : 0;
+    h->prox_on = prox_on ? 1 : 0;
+    return 0;
+}
+
+extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
+                           double* y, double* obj, double* bound, int32_t* status,
+                           int32_t* iters, void* stream) {
+    if (!h) return set_err(-1, "null handle");
+    if (!x || !obj || !bound || !status) return set_err(-1, "null output pointer");
+    phgpu_options o;
+    if (opt) o = *opt;
+    else phgpu_default_options(&o);
+    if (o.check_every < 1 || o.max_iter < 1 || !(o.eta_frac > 0.0 && o.eta_frac < 1.0) ||
+        o.gamma < 0.0 || o.gamma > 1.0)
+        return set_err(-1, "bad options (check_every=%d max_iter=%d eta_frac=%g gamma=%g)",
+                       o.check_every, o.max_iter, o.eta_frac, o.gamma);
+    solve_params P;
+    P.eps_rel = o.eps_rel;
+    P.eps_abs = o.eps_abs;
+    P.gamma = o.gamma;
+    P.bsuff = o.beta_sufficient;
+    P.bnec = o.beta_necessary;
+    P.eta_frac = o.eta_frac;
+    P.omega0 = o.omega0;
+    P.max_iter = o.max_iter;
+    P.check_every = o.check_every;
+    P.warm = (warm_start && h->have_solution) ? 1 : 0;
+    P.keep_omega = o.keep_omega;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+    HIPCHK(hipGetLastError());
+    h->have_solution = 1;
+    return 0;
+}
+
+extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
+    if (!h || !x || !node_buf) return set_err(-1, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
+    HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
+    if (h->nn == 0) return 0;
+    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_xbar_final, dim3((h->nn + 63) / 64), dim3(64), 0, st, *h, node_buf);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf,
+                               double* xbar, double* W, const double* rho, int update_W,
+                               double* conv_local, void* stream) {
+    if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
+        return set_err(-1, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_ph_update, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, xbar, W, rho,
+                       update_W ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    const double scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)h->part, h->nwaves, 1,
+                       scale, conv_local);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
+                                  const int32_t* status, double* out, void* stream) {
+    if (!h || !obj || !bound || !status || !out) return set_err(-1, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_expect_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, obj, bound, status);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_sum_partials, dim3(4), dim3(256), 0, st, (const double*)h->part, h->nwaves, 4, 1.0,
+                       out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_destroy(phgpu_handle h) {
+    if (!h) return 0;
+    void* ptrs[] = {h->row_ptr, h->col_idx, h->col_ptr, h->row_idx, h->perm, h->row_of,
+                    h->nonant_col, h->nonant_depth, h->nonant_off, h->nonant_slot,
+                    h->A, h->c, h->lb, h->ub, h->q, h->rl, h->ru, h->objc, h->prob, h->pcoef,
+                    h->node_of, h->Ah_csr, h->Ah_csc, h->Dr, h->Dc, h->normA, h->lbh, h->ubh,
+                    h->rlh, h->ruh, h->ch, h->qh, h->x, h->x0, h->xe, h->xt, h->aty, h->aty0,
+                    h->y, h->y0, h->yt, h->omega, h->part, h->part_node};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete h;
+    return 0;
+}
+
+extern "C" int phgpu_last_error(char* buf, size_t len) {
+    if (!buf || len == 0) return -1;
+    strncpy(buf, g_err, len - 1);
+    buf[len - 1] = 0;
+    return 0;
+}
+
+extern "C" int64_t phgpu_workspace_bytes(phgpu_handle h) { return h ? h->ws_bytes : -1; }

@@ -1,0 +1,205 @@
+"""Device engine: one rank's ScenarioBatch resident in HBM + the libphgpu calls.
+
+Owns the caller-side device buffers of include/phgpu.h (torch tensors on the rank's
+GPU, scenario-fastest ``[k, S]``) and sequences the per-PH-iteration work:
+
+    solve_loop      -> phgpu_solve                     (spopt.py:226-307)
+    Compute_Xbar    -> phgpu_ph_reduce + all-reduce    (phbase.py:27-107)
+    Update_W + conv -> phgpu_ph_update + all-reduce    (phbase.py:293-343)
+    Ebound/Eobj/E1  -> phgpu_expectations + all-reduce (spopt.py:310-439)
+
+All launches go to torch's current stream; host synchronisation happens only where
+the reference needs a host scalar (the convergence test, bounds).
+"""
+import ctypes
+import numpy as np
+import torch
+
+from . import _lib
+from .comm import Comm
+
+
+def _dev_T(a, device, dtype=torch.float64):
+    """host [S, k] -> device [k, S] contiguous."""
+    a = np.asarray(a)
+    if a.ndim == 1:
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dtype)
+    return torch.from_numpy(np.ascontiguousarray(a.T)).to(device=device, dtype=dtype)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def combine_node_partials(comm, node_buf):
+    """Cross-rank sum of the node-indexed x̄ / x̄² partial buffer (phbase.py:83-87)."""
+    return comm.allreduce_sum_(node_buf)
+
+
+class PHEngine:
+    def __init__(self, batch, device=None, comm=None, node_names=None):
+        if not torch.cuda.is_available():
+            raise _lib.PhgpuError("PHEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _lib.load()
+        self.batch = batch
+        self.comm = comm or Comm()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        b = batch
+        S, n, m, nn = b.S, b.n, b.m, b.nn
+        self.S, self.n, self.m, self.nn = S, n, m, nn
+        # global node numbering (identical on all ranks): node_names of the PH object
+        names = node_names if node_names is not None else b.node_names
+        gid = {nd: i for i, nd in enumerate(names)}
+        remap = np.array([gid[nd] for nd in b.node_names], dtype=np.int32)
+        node_of = remap[b.node_of]
+        self.node_names = list(names)
+        self.num_nodes = len(names)
+        self.nlen_max = max(1, b.nlen_max)
+        h = ctypes.c_void_p()
+        rp = np.ascontiguousarray(b.row_ptr, dtype=np.int32)
+        ci = np.ascontiguousarray(b.col_idx, dtype=np.int32)
+        nc = np.ascontiguousarray(b.nonant_col, dtype=np.int32)
+        nd = np.ascontiguousarray(b.nonant_depth, dtype=np.int32)
+        no = np.ascontiguousarray(b.nonant_off, dtype=np.int32)
+        P = lambda a: a.ctypes.data_as(_lib.P_i32)  # noqa: E731
+        torch.cuda.set_device(self.dev_index)
+        _lib.check(self.lib.phgpu_create(ctypes.byref(h), self.dev_index, S, n, m, b.nnz, P(rp), P(ci),
+                                         nn, P(nc), P(nd), P(no), b.depth, self.num_nodes,
+                                         self.nlen_max), "phgpu_create")
+        self.h = h
+        dev = self.device
+        self.A_val = _dev_T(b.A_val, dev)
+        self.c = _dev_T(b.c, dev)
+        self.lb = _dev_T(b.lb, dev)
+        self.ub = _dev_T(b.ub, dev)
+        self.rl = _dev_T(b.rl, dev)
+        self.ru = _dev_T(b.ru, dev)
+        self.q = _dev_T(b.q, dev)
+        self.obj_const = _dev_T(b.obj_const, dev)
+        self.prob = _dev_T(b.prob, dev)
+        self.node_of = _dev_T(node_of, dev, torch.int32)
+        self.prob_coeff = _dev_T(b.prob_coeff, dev)
+        # caller-owned I/O buffers
+        z = lambda *s: torch.zeros(*s, dtype=torch.float64, device=dev)  # noqa: E731
+        self.x = z(n, S)
+        self.y = z(max(m, 1), S)
+        self.obj = z(S)
+        self.bound = z(S)
+        self.status = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.iters = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.W = z(max(nn, 1), S)
+        self.rho = z(max(nn, 1), S)
+        self.xbar = z(max(nn, 1), S)
+        self.node_buf = z(2 * self.num_nodes * self.nlen_max)
+        self.conv_buf = z(1)
+        self.exp_buf = z(4)
+        self.W_on = 0
+        self.prox_on = 0
+        self._upload()
+
+    # -------------------------------------------------------------- plumbing
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _upload(self):
+        _lib.check(self.lib.phgpu_set_scenarios(
+            self.h, _ptr(self.A_val), _ptr(self.c), _ptr(self.lb), _ptr(self.ub), _ptr(self.rl),
+            _ptr(self.ru), _ptr(self.q), _ptr(self.obj_const), _ptr(self.prob), _ptr(self.node_of),
+            _ptr(self.prob_coeff), self._stream()), "phgpu_set_scenarios")
+        self._bind()
+
+    def _bind(self):
+        _lib.check(self.lib.phgpu_set_ph_state(self.h, _ptr(self.W), _ptr(self.rho), _ptr(self.xbar),
+                                               self.W_on, self.prox_on), "phgpu_set_ph_state")
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            torch.cuda.synchronize(self.device)
+            self.lib.phgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def workspace_bytes(self):
+        return int(self.lib.phgpu_workspace_bytes(self.h))
+
+    # -------------------------------------------------------------- PH state
+    def set_rho(self, rho):
+        """rho: scalar or host [S, nn] array (the rho Params of phbase.py:598-602)."""
+        if np.isscalar(rho):
+            self.rho.fill_(float(rho))
+        else:
+            self.rho.copy_(_dev_T(np.asarray(rho, dtype=np.float64), self.device))
+
+    def set_W(self, W):
+        self.W.copy_(_dev_T(np.asarray(W, dtype=np.float64), self.device))
+
+    def set_xbar(self, xbar):
+        self.xbar.copy_(_dev_T(np.asarray(xbar, dtype=np.float64), self.device))
+
+    def set_terms(self, W_on, prox_on):
+        self.W_on = 1 if W_on else 0
+        self.prox_on = 1 if prox_on else 0
+        self._bind()
+
+    # -------------------------------------------------------------- hot path
+    def solve(self, options=None, warm=True):
+        o = options if options is not None else _lib.default_options()
+        _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(self.x),
+                                        _ptr(self.y), _ptr(self.obj), _ptr(self.bound),
+                                        _ptr(self.status), _ptr(self.iters), self._stream()),
+                   "phgpu_solve")
+
+    def compute_xbar_partials(self):
+        _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),
+                   "phgpu_ph_reduce")
+        return self.node_buf
+
+    def compute_xbar(self):
+        """Local partials + cross-rank sum (phbase.py:27-87); result left in node_buf."""
+        self.compute_xbar_partials()
+        combine_node_partials(self.comm, self.node_buf)
+        return self.node_buf
+
+    def update(self, update_W=True):
+        """Scatter x̄, W += rho (x - x̄), local conv (phbase.py:90-103, 293-339)."""
+        _lib.check(self.lib.phgpu_ph_update(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
+                                            _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
+                                            _ptr(self.conv_buf), self._stream()), "phgpu_ph_update")
+
+    def convergence_diff(self):
+        """phbase.py:330-343: sum over ranks of per-rank means, / n_proc (host float)."""
+        self.comm.allreduce_sum_(self.conv_buf)
+        return float(self.conv_buf.item()) / self.comm.size
+
+    def expectations(self):
+        """(Eobj, Ebound, E1, Efeas) summed over ranks (spopt.py:310-439)."""
+        _lib.check(self.lib.phgpu_expectations(self.h, _ptr(self.obj), _ptr(self.bound), _ptr(self.status),
+                                               _ptr(self.exp_buf), self._stream()), "phgpu_expectations")
+        self.comm.allreduce_sum_(self.exp_buf)
+        v = self.exp_buf.cpu().numpy()
+        return float(v[0]), float(v[1]), float(v[2]), float(v[3])
+
+    # -------------------------------------------------------------- host views
+    def nonant_x(self):
+        """[S, nn] host array of the nonant values (W cache 'ci' order, phbase.py:355-365)."""
+        idx = torch.as_tensor(self.batch.nonant_col, dtype=torch.long, device=self.device)
+        return self.x.index_select(0, idx).T.cpu().numpy()
+
+    def host(self, name):
+        t = getattr(self, name)
+        a = t.cpu().numpy()
+        return a.T if a.ndim == 2 else a
+
+    def node_xbar(self):
+        """{node name: x̄ vector} from the (reduced) node buffer."""
+        buf = self.node_buf.cpu().numpy()
+        nl = self.nlen_max
+        return {nd: buf[g * nl:(g + 1) * nl] for g, nd in enumerate(self.node_names)}

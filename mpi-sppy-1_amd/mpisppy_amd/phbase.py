@@ -1,0 +1,273 @@
+"""PHBase: the progressive-hedging algorithm on the batched engine (mirrors mpisppy/phbase.py).
+
+Same constructor (phbase.py:235-249), required options (phbase.py:732-752), method
+names and loop order (Iter0 758-872; iterk_loop 875-979: x̄ -> W -> conv -> break? ->
+solve -> sync).  The per-scenario Python loops become device kernels:
+
+  Compute_Xbar      -> phgpu_ph_reduce + one all-reduce of the node buffer
+  Update_W + conv   -> phgpu_ph_update (one fused kernel) + one scalar all-reduce
+  solve_loop        -> phgpu_solve over all local scenarios
+"""
+import time
+import numpy as np
+
+from . import global_toc
+from .spopt import SPOpt
+
+
+class PHBase(SPOpt):
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None, extensions=None,
+                 extension_kwargs=None, ph_converger=None, rho_setter=None,
+                 variable_probability=None):
+        self.start_time = time.perf_counter()
+        super().__init__(options, all_scenario_names, scenario_creator,
+                         scenario_denouement=scenario_denouement, all_nodenames=all_nodenames,
+                         mpicomm=mpicomm, extensions=extensions, extension_kwargs=extension_kwargs,
+                         scenario_creator_kwargs=scenario_creator_kwargs,
+                         variable_probability=variable_probability)
+        global_toc("Initializing PHBase", self.cylinder_rank == 0 and options.get("toc", True))
+        self.options = options
+        self.options_check()
+        self.ph_converger = ph_converger
+        self.rho_setter = rho_setter
+        self.iter0_solver_options = options.get("iter0_solver_options") or {}
+        self.iterk_solver_options = options.get("iterk_solver_options") or {}
+        self.current_solver_options = self.iter0_solver_options
+        self.convobject = None
+        self.conv = None
+        self._PHIter = 0
+        self.iter_times = []
+
+    # phbase.py:732-752
+    def options_check(self):
+        required = ["solver_name", "PHIterLimit", "defaultPHrho", "convthresh", "verbose",
+                    "display_progress"]
+        self._options_check(required, self.options)
+        self.options.setdefault("display_timing", False)
+        self.options.setdefault("display_convergence_detail", False)
+
+    # phbase.py:585-602 + 1040-1050 (W = 0, rho = defaultPHrho, x̄ = 0, terms off)
+    def attach_Ws_and_prox(self):
+        self._create_solvers()
+        e = self.engine
+        e.W.zero_()
+        e.xbar.zero_()
+        e.set_rho(float(self.options["defaultPHrho"]))
+        e.set_terms(0, 0)
+
+    def PH_Prep(self, attach_duals=True, attach_prox=True):
+        """phbase.py:702-716."""
+        self._attach_duals = attach_duals
+        self._attach_prox = attach_prox
+        self.attach_Ws_and_prox()
+
+    # W_on / prox_on toggles (phbase.py:408-437)
+    @property
+    def W_disabled(self):
+        return not bool(self.engine.W_on)
+
+    @property
+    def prox_disabled(self):
+        return not bool(self.engine.prox_on)
+
+    def _disable_W(self):
+        self.engine.set_terms(0, self.engine.prox_on)
+
+    def _disable_prox(self):
+        self.engine.set_terms(self.engine.W_on, 0)
+
+    def _reenable_W(self):
+        self.engine.set_terms(1 if getattr(self, "_attach_duals", True) else 0, self.engine.prox_on)
+
+    def _reenable_prox(self):
+        self.engine.set_terms(self.engine.W_on, 1 if getattr(self, "_attach_prox", True) else 0)
+
+    def disable_W_and_prox(self):
+        self.engine.set_terms(0, 0)
+
+    def reenable_W_and_prox(self):
+        self._reenable_W()
+        self._reenable_prox()
+
+    # phbase.py:494-568 (dis_W / dis_prox wrappers around SPOpt.solve_loop)
+    def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
+                   dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
+                   tee=False, verbose=False, warm_start=True):
+        wo, po = self.engine.W_on, self.engine.prox_on
+        if dis_W or dis_prox:
+            self.engine.set_terms(0 if dis_W else wo, 0 if dis_prox else po)
+        super().solve_loop(solver_options, use_scenarios_not_subproblems, dtiming, gripe,
+                           disable_pyomo_signal_handling, tee, verbose, warm_start=warm_start)
+        if dis_W or dis_prox:
+            self.engine.set_terms(wo, po)
+
+    # phbase.py:27-107 / 265-291
+    def Compute_Xbar(self, verbose=False):
+        self.engine.compute_xbar()
+
+    # phbase.py:293-318 (fused with the x̄ scatter and the conv partial sum)
+    def Update_W(self, verbose=False):
+        self.engine.update(update_W=True)
+
+    # phbase.py:321-343
+    def convergence_diff(self):
+        return self.engine.convergence_diff()
+
+    # phbase.py:346-385 -- "ci" order = local scenarios x nonant order
+    def _populate_W_cache(self, cache, padding):
+        W = self.engine.host("W")[:, :self.batch.nn]
+        flat = W.reshape(-1)
+        if len(flat) + padding != len(cache):
+            raise RuntimeError("W cache length mismatch")
+        cache[:len(flat)] = flat
+
+    def W_from_flat_list(self, flat_list):
+        S, nn = self.batch.S, self.batch.nn
+        self.engine.set_W(np.asarray(flat_list[:S * nn], dtype=np.float64).reshape(S, nn))
+
+    # phbase.py:387-406
+    def _use_rho_setter(self, verbose):
+        if self.rho_setter is None:
+            return
+        if not self.local_scenarios:
+            raise RuntimeError("rho_setter needs per-scenario models; pass options['rho_array'] with a batch_creator")
+        kw = self.options.get("rho_setter_kwargs", {})
+        rho = self.engine.host("rho")[:, :self.batch.nn].copy()
+        for s, nm in enumerate(self.local_scenario_names):
+            mdl = self.local_scenarios[nm]
+            id2k = {}
+            k = 0
+            for nd in mdl._mpisppy_node_list:
+                for v in nd.nonant_vardata_list:
+                    id2k[id(v)] = k
+                    k += 1
+            for (vid, r) in self.rho_setter(mdl, **kw):
+                rho[s, id2k[vid]] = r
+        self.engine.set_rho(rho)
+
+    # phbase.py:758-872
+    def Iter0(self):
+        if self.extensions is not None and hasattr(self.extobject, "pre_iter0"):
+            self.extobject.pre_iter0()
+        verbose = self.options["verbose"]
+        dprogress = self.options["display_progress"]
+        dtiming = self.options["display_timing"]
+        self._PHIter = 0
+        global_toc("Creating solvers", self.cylinder_rank == 0 and self.options.get("toc", True))
+        self._create_solvers()
+        global_toc("Entering solve loop in PHBase.Iter0", self.cylinder_rank == 0 and self.options.get("toc", True))
+        self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
+                        verbose=verbose, warm_start=False)
+        self._update_E1()
+        if abs(1 - self.E1) > self.E1_tolerance:
+            # the reference prints ERROR and calls quit() (phbase.py:812-817)
+            raise RuntimeError(f"Total probability of scenarios was {self.E1} "
+                               f"(E1_tolerance = {self.E1_tolerance})")
+        feasP = self.feas_prob()
+        if abs(feasP - self.E1) > 1e-12 * max(1.0, abs(self.E1)):
+            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1}")  # :818-823
+        if self.extensions is not None and hasattr(self.extobject, "post_iter0"):
+            self.extobject.post_iter0()
+        if self.spcomm is not None:
+            self.spcomm.sync()
+        if self.extensions is not None and hasattr(self.extobject, "post_iter0_after_sync"):
+            self.extobject.post_iter0_after_sync()
+        if self.rho_setter is not None:
+            self._use_rho_setter(verbose and self.cylinder_rank == 0)
+        if "rho_array" in self.options:
+            self.engine.set_rho(self.options["rho_array"])
+        if self.ph_converger is not None:
+            self.convobject = self.ph_converger(self)
+        self.conv = None
+        self.trivial_bound = self.Ebound(verbose)
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("After PH Iteration", self._PHIter)
+            print("Trivial bound =", self.trivial_bound)
+            print("PHBase Convergence Metric =", self.conv)
+            print("Elapsed time: %6.2f" % (time.perf_counter() - self.start_time))
+        self.reenable_W_and_prox()
+        self.current_solver_options = self.iterk_solver_options
+        return self.trivial_bound
+
+    # phbase.py:875-979
+    def iterk_loop(self):
+        verbose = self.options["verbose"]
+        have_ext = self.extensions is not None
+        dprogress = self.options["display_progress"]
+        dtiming = self.options["display_timing"]
+        self.conv = None
+        max_iterations = int(self.options["PHIterLimit"])
+        self.converged = False
+        for self._PHIter in range(1, max_iterations + 1):
+            t0 = time.perf_counter()
+            if dprogress:
+                global_toc(f"\nInitiating PH Iteration {self._PHIter}\n", self.cylinder_rank == 0)
+            self.Compute_Xbar(verbose)
+            self.Update_W(verbose)
+            self.conv = self.convergence_diff()
+            if have_ext and hasattr(self.extobject, "miditer"):
+                self.extobject.miditer()
+            if self.ph_converger is not None:
+                if self.convobject.is_converged():
+                    self.converged = True
+                    global_toc("User-supplied converger determined termination criterion reached",
+                               self.cylinder_rank == 0)
+                    break
+            elif self.conv is not None and self.conv < self.options["convthresh"]:
+                self.converged = True
+                global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
+                           % (self.conv, self.options["convthresh"]), self.cylinder_rank == 0)
+                break
+            self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
+                            verbose=verbose)
+            if have_ext and hasattr(self.extobject, "enditer"):
+                self.extobject.enditer()
+            if self.spcomm is not None:
+                self.spcomm.sync()
+                if self.spcomm.is_converged():
+                    global_toc("Cylinder convergence", self.cylinder_rank == 0)
+                    break
+            if have_ext and hasattr(self.extobject, "enditer_after_sync"):
+                self.extobject.enditer_after_sync()
+            self.iter_times.append(time.perf_counter() - t0)
+            if dprogress and self.cylinder_rank == 0:
+                print("")
+                print("After PH Iteration", self._PHIter)
+                print("Scaled PHBase Convergence Metric=", self.conv)
+                print("Iteration time: %6.2f" % (time.perf_counter() - t0))
+                print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
+        else:
+            self.mpicomm.Barrier()
+            global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations,
+                       self.cylinder_rank == 0)
+
+    # phbase.py:982-1037
+    def post_loops(self, extensions=None):
+        dprogress = self.options["display_progress"]
+        self.mpicomm.Barrier()
+        if self.scenario_denouement is not None and self.local_scenarios:
+            self.load_solutions_to_models()
+            for sname, s in self.local_scenarios.items():
+                self.scenario_denouement(self.cylinder_rank, sname, s)
+        self.mpicomm.Barrier()
+        if extensions is not None and hasattr(self.extobject, "post_everything"):
+            self.extobject.post_everything()
+        Eobj = self.Eobjective()
+        self.mpicomm.Barrier()
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("Current ***weighted*** E[objective] =", Eobj)
+            print("")
+        return Eobj
+
+    # -- host views used by tests / writers
+    def xbar_by_node(self):
+        return self.engine.node_xbar()
+
+    def W_array(self):
+        return self.engine.host("W")[:, :self.batch.nn]
+
+    def nonants_array(self):
+        return self.engine.nonant_x()

@@ -1,0 +1,102 @@
+"""SPBase: scenario creation, rank partition, tree bookkeeping (mirrors mpisppy/spbase.py).
+
+Constructor signature and attribute names follow spbase.py:44-120.  What changes is
+the storage: instead of one Pyomo model per local scenario, the local scenarios are
+one :class:`ScenarioBatch` (shared CSR pattern + per-scenario arrays), built either
+
+  * from ``options["batch_creator"](local_names, **scenario_creator_kwargs)``
+    (vectorised; used for the 65,536-scenario configurations), or
+  * from ``scenario_creator(name, **kwargs)`` per local name, exactly like
+    SPBase._create_scenarios (spbase.py:255-291); those LinearModels are kept in
+    ``local_scenarios`` so values can be loaded back into them.
+"""
+import numpy as np
+
+from . import global_toc
+from .batch import batch_from_models
+from .comm import Comm
+from .sputils import rank_slices
+
+
+def nonleaf_nodenames(all_nodenames):
+    """Non-leaf nodes in all_nodenames order (a node is a leaf when it has no child
+    '<name>_0', sputils.find_leaves 659-670); two-stage = ['ROOT']."""
+    if all_nodenames is None or all_nodenames == ["ROOT"]:
+        return ["ROOT"]
+    s = set(all_nodenames)
+    return [nd for nd in all_nodenames if nd + "_0" in s]
+
+
+class SPBase:
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None,
+                 variable_probability=None, E1_tolerance=1e-5):
+        self.options = options
+        self.all_scenario_names = list(all_scenario_names)
+        self.scenario_creator = scenario_creator
+        self.scenario_denouement = scenario_denouement
+        self.E1_tolerance = E1_tolerance
+        if all_nodenames is None:
+            self.all_nodenames = ["ROOT"]
+        elif "ROOT" in all_nodenames:
+            self.all_nodenames = list(all_nodenames)
+        else:
+            raise RuntimeError("'ROOT' must be in the list of node names")
+        if variable_probability is not None:
+            raise NotImplementedError("variable_probability is outside the batched PH hot path")
+        self.multistage = len(self.all_nodenames) > 1
+        self.mpicomm = mpicomm if mpicomm is not None else Comm()
+        self.cylinder_rank = self.mpicomm.Get_rank()
+        self.n_proc = self.mpicomm.Get_size()
+        self.global_rank = self.cylinder_rank
+        if options.get("toc", True):
+            global_toc("Initializing SPBase", self.cylinder_rank == 0)
+        if self.n_proc > len(self.all_scenario_names):
+            raise RuntimeError("More ranks than scenarios")                 # spbase.py:94-95
+        if options.get("bundles_per_rank", 0):
+            raise NotImplementedError("bundles are outside the batched PH hot path")
+        self.bundling = False
+        # rank slices (sputils.py:798-810 via spbase.py:184-216)
+        self._rank_slices = rank_slices(len(self.all_scenario_names), self.n_proc)
+        self.local_scenario_names = [self.all_scenario_names[i]
+                                     for i in self._rank_slices[self.cylinder_rank]]
+        self.node_names = nonleaf_nodenames(self.all_nodenames)
+        self.scenario_creator_kwargs = scenario_creator_kwargs or {}
+        self._create_scenarios()
+
+    def _create_scenarios(self):
+        kw = self.scenario_creator_kwargs
+        bc = self.options.get("batch_creator")
+        num_all = len(self.all_scenario_names)
+        if bc is not None:
+            self.local_scenarios = {}
+            self.batch = bc(self.local_scenario_names, **kw)
+            # uniform default probability when the creator gives none (spbase.py:515-520)
+            if np.any(~np.isfinite(self.batch.prob)):
+                self.batch.prob[:] = 1.0 / num_all
+        else:
+            models = [self.scenario_creator(nm, **kw) for nm in self.local_scenario_names]
+            self.local_scenarios = dict(zip(self.local_scenario_names, models))
+            for nm, mdl in self.local_scenarios.items():
+                if mdl._mpisppy_node_list is None:
+                    raise RuntimeError(f"_mpisppy_node_list not found on scenario {nm}")
+                if mdl._mpisppy_probability is None and self.cylinder_rank == 0 and nm == self.local_scenario_names[0]:
+                    print(f"Did not find _mpisppy_probability, assuming uniform probability {1.0 / num_all}")
+            self.batch = batch_from_models(self.local_scenario_names, models,
+                                           all_nodenames=self.all_nodenames, num_all_scens=num_all,
+                                           node_names=self.node_names if self.multistage else None)
+        for nd in self.batch.node_names:
+            if nd not in self.node_names:
+                raise RuntimeError(f"Tree node '{nd}' not in all_nodenames list {self.all_nodenames}")
+        self.is_minimizing = self.batch.sense > 0
+        self.nonant_length = self.batch.nn
+        self.scenarios_constructed = True
+
+    @property
+    def local_subproblems(self):
+        return self.local_scenarios
+
+    def _options_check(self, required_options, given_options):
+        missing = [o for o in required_options if o not in given_options]
+        if missing:
+            raise ValueError(f"Missing option(s) {missing}")

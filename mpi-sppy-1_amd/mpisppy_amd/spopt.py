@@ -1,0 +1,113 @@
+"""SPOpt: the batched solve loop and expectations (mirrors mpisppy/spopt.py).
+
+``solve_loop`` keeps the reference's signature (spopt.py:226-233) but replaces the
+per-scenario ``solve_one`` + SolverFactory plugin call (spopt.py:85-223) with ONE
+``phgpu_solve`` over all local scenarios.  Solver selection is by ``solver_name``
+(cfg_vanilla.py:43 -> spopt.py:844): this engine answers to ``"mi355x_pdhg"``
+(aliases below).  ``iter0_solver_options`` / ``iterk_solver_options`` keys are the
+fields of ``phgpu_options`` (include/phgpu.h).
+
+Documented limitation: per-scenario extension hooks ``pre_solve`` / ``post_solve``
+cannot run inside a batched solve; ``pre_solve_loop`` / ``post_solve_loop`` do.
+"""
+import time
+import numpy as np
+
+from . import _lib
+from .spbase import SPBase
+from .engine import PHEngine
+
+SOLVER_NAMES = ("mi355x_pdhg", "phgpu", "mi355x")
+
+
+class SPOpt(SPBase):
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, extensions=None, extension_kwargs=None,
+                 scenario_creator_kwargs=None, variable_probability=None, E1_tolerance=1e-5):
+        super().__init__(options, all_scenario_names, scenario_creator, scenario_denouement,
+                         all_nodenames, mpicomm, scenario_creator_kwargs, variable_probability,
+                         E1_tolerance)
+        self.extensions = extensions
+        self.extension_kwargs = extension_kwargs
+        if extensions is not None:
+            self.extobject = extensions(self) if extension_kwargs is None else extensions(self, **extension_kwargs)
+        self.spcomm = None
+        self.engine = None
+        self.solve_times = []
+        self.pdhg_iters = []
+
+    # spopt.py:839-868
+    def _create_solvers(self):
+        sname = self.options.get("solver_name")
+        if sname not in SOLVER_NAMES:
+            raise RuntimeError(f"solver_name {sname!r} is not served by this engine; use one of {SOLVER_NAMES}")
+        if self.engine is None:
+            self.engine = PHEngine(self.batch, device=self.options.get("device"), comm=self.mpicomm,
+                                   node_names=self.node_names)
+
+    @staticmethod
+    def _to_phgpu_options(solver_options):
+        return _lib.default_options(**(solver_options or {}))
+
+    # spopt.py:226-307
+    def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
+                   gripe=False, disable_pyomo_signal_handling=False, tee=False, verbose=False,
+                   warm_start=True):
+        if self.extensions is not None and hasattr(self.extobject, "pre_solve_loop"):
+            self.extobject.pre_solve_loop()
+        t0 = time.perf_counter()
+        self.engine.solve(self._to_phgpu_options(solver_options), warm=warm_start)
+        if dtiming or self.options.get("record_pdhg_iters", False):
+            import torch
+            torch.cuda.synchronize()
+            it = self.engine.iters.cpu().numpy()
+            self.pdhg_iters.append((int(it.max()), float(it.mean())))
+        self.solve_times.append(time.perf_counter() - t0)
+        if self.extensions is not None and hasattr(self.extobject, "post_solve_loop"):
+            self.extobject.post_solve_loop()
+        if dtiming and self.cylinder_rank == 0:
+            print("Batched solve time (seconds): %4.4f  PDHG iters max/mean %d/%.1f"
+                  % (self.solve_times[-1], *self.pdhg_iters[-1]))
+        if gripe:
+            st = self.engine.status.cpu().numpy()
+            bad = np.nonzero(st != _lib.OPTIMAL)[0]
+            for k in bad[:10]:
+                print(f"Solve failed for scenario {self.batch.names[k]} (status {st[k]})")
+
+    # spopt.py:310-343 ("weighted, proxed" objective, phbase.py:991)
+    def Eobjective(self, verbose=False):
+        e = self.engine.expectations()
+        return self.batch.sense * e[0]
+
+    # spopt.py:346-391
+    def Ebound(self, verbose=False, extra_sum_terms=None):
+        e = self.engine.expectations()
+        b = self.batch.sense * e[1]
+        if extra_sum_terms is not None:
+            import torch
+            t = torch.tensor(list(extra_sum_terms), dtype=torch.float64, device=self.engine.device)
+            self.mpicomm.allreduce_sum_(t)
+            return b, t.cpu().numpy()
+        return b
+
+    # spopt.py:394-408
+    def _update_E1(self):
+        self.E1 = self.engine.expectations()[2]
+
+    # spopt.py:411-439
+    def feas_prob(self):
+        return self.engine.expectations()[3]
+
+    def infeas_prob(self):
+        e = self.engine.expectations()
+        return e[2] - e[3]
+
+    # -- values back into the LinearModels (for denouement / writers)
+    def load_solutions_to_models(self):
+        if not self.local_scenarios:
+            return
+        x = self.engine.host("x")  # [S, n]
+        for s, nm in enumerate(self.local_scenario_names):
+            mdl = self.local_scenarios[nm]
+            for j, v in enumerate(mdl.vars):
+                v._value = float(x[s, j])

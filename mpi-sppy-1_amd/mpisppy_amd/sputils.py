@@ -1,0 +1,84 @@
+"""Scenario-tree and naming utilities (mirrors mpisppy/utils/sputils.py).
+
+Only what the PH hot path needs: ``extract_num`` (sputils.py:481-490), the balanced
+tree helpers (``node_idx`` 494-519, ``_nodenum_before_stage`` 654-657,
+``create_nodenames_from_branching_factors`` 934-959), ``attach_root_node``
+(844-860) and the rank partition of ``_ScenTree.scen_names_to_ranks`` (774-840).
+"""
+import re
+import numpy as np
+
+from .scenario_tree import ScenarioNode
+
+
+def extract_num(string):
+    """Longest run of digits at the right end of ``string`` (sputils.py:481-490)."""
+    return int(re.compile(r"(\d+)$").search(string).group(1))
+
+
+def _nodenum_before_stage(t, branching_factors):
+    return int(sum(np.prod(branching_factors[0:i]) for i in range(t)))
+
+
+def node_idx(node_path, branching_factors):
+    if node_path == []:
+        return 0
+    stage_id = 0
+    for t in range(len(node_path)):
+        stage_id = node_path[t] + branching_factors[t] * stage_id
+    return _nodenum_before_stage(len(node_path), branching_factors) + stage_id
+
+
+def create_nodenames_from_branching_factors(BFS):
+    stage_nodes = ["ROOT"]
+    nodenames = ["ROOT"]
+    if len(BFS) == 1:
+        return nodenames
+    for bf in BFS:
+        old = stage_nodes
+        stage_nodes = []
+        for k in range(len(old)):
+            stage_nodes += ["%s_%i" % (old[k], b) for b in range(bf)]
+        nodenames += stage_nodes
+    return nodenames
+
+
+def attach_root_node(model, firstobj, varlist, nonant_ef_suppl_list=None):
+    """sputils.py:844-860: a two-stage scenario has the single node ROOT."""
+    model._mpisppy_node_list = [
+        ScenarioNode("ROOT", 1.0, 1, firstobj, varlist, model,
+                     nonant_ef_suppl_list=nonant_ef_suppl_list)
+    ]
+
+
+def rank_slices(num_scens, n_proc):
+    """Contiguous scenario slices per rank, sputils.py:798-810 (n_proc == 1 special
+    case 798-801; ``range(int(i*avg), int((i+1)*avg))`` otherwise)."""
+    if n_proc == 1:
+        return [list(range(num_scens))]
+    avg = num_scens / n_proc
+    return [list(range(int(i * avg), int((i + 1) * avg))) for i in range(n_proc)]
+
+
+def option_string_to_dict(ostr):
+    """sputils.option_string_to_dict: 'a=1 b' -> {'a': 1.0, 'b': None}."""
+    def convert_value_string_to_number(s):
+        try:
+            return int(s)
+        except ValueError:
+            try:
+                return float(s)
+            except ValueError:
+                return s
+    solver_options = dict()
+    if ostr is None or ostr == "":
+        return solver_options
+    for this_option_string in ostr.split():
+        this_option_pieces = this_option_string.strip().split("=")
+        if len(this_option_pieces) == 2:
+            solver_options[this_option_pieces[0]] = convert_value_string_to_number(this_option_pieces[1])
+        elif len(this_option_pieces) == 1:
+            solver_options[this_option_pieces[0]] = None
+        else:
+            raise RuntimeError("Illegally formed subsolve directive option=%s detected" % this_option_string)
+    return solver_options
