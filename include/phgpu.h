@@ -68,7 +68,9 @@ typedef struct {
     double eta_frac;       /* step = eta_frac / ||A_scaled||_2                [0.998] */
     double omega0;         /* initial primal weight (<= 0: keep previous)     [1.0] */
     int32_t keep_omega;    /* 1: carry the primal weight across solves         [1] */
-    int32_t reserved;
+    int32_t restart_every; /* restart test period (iterations; divides check_every) [16] */
+    double beta_artificial;/* restart when the Halpern run exceeds this fraction
+                              of all iterations of the solve                  [0.36] */
 } phgpu_options;
 
 /* Fill *opt with the defaults shown above. */
@@ -141,7 +143,9 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
 
 /* Local probability-weighted sums (spopt.py:310-439) into out[4]:
  *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
- *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s: status==OPTIMAL} prob_s */
+ *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s feasible} prob_s, where feasible
+ *   means status is OPTIMAL or ITER_LIMIT (a solution was loaded; spopt.py:175-194
+ *   marks only infeasible / unbounded / no-solution results infeasible) */
 int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
                        const int32_t* status, double* out, void* stream);
 

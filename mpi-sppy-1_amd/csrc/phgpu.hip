@@ -195,8 +195,8 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
 
 // ------------------------------------------------------------------ solve kernel
 struct solve_params {
-    double eps_rel, eps_abs, gamma, bsuff, bnec, eta_frac, omega0;
-    int max_iter, check_every, warm, keep_omega;
+    double eps_rel, eps_abs, gamma, bsuff, bnec, bart, eta_frac, omega0;
+    int max_iter, check_every, restart_every, warm, keep_omega;
 };
 
 __global__ void __launch_bounds__(BLOCK)
@@ -284,7 +284,9 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     bool final_is_t = false;  // true: solution is T(z) (in xt/yt/xe)
     for (; it < P.max_iter; ++it) {
         const double tau = eta / omega, sig = eta * omega;
-        const bool check = (it % P.check_every) == 0;
+        const bool kkt = (it % P.check_every) == 0;
+        // non-fused iteration (T(z) kept in xt / yt / xe) at restart-test points
+        const bool check = kkt || (it % P.restart_every) == 0;
         const double a1 = (hk + 1.0) / (hk + 2.0), a0 = 1.0 / (hk + 2.0);
         double dx2 = 0.0, dy2 = 0.0;
         // --- primal step: xt = prox(x - tau (c - A^T y)); xe = 2 xt - x
@@ -323,6 +325,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             continue;
         }
         // ---- KKT test on T(z) = (xt, yt), original space
+        if (kkt) {
         double pres2 = 0.0, dres2 = 0.0;
         pobj = const_term;
         dobj = const_term;
@@ -361,8 +364,11 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             final_is_t = true;
             break;
         }
-        // ---- restart test (cuPDLP+-style: sufficient / necessary-without-progress)
-        const bool restart = (r <= P.bsuff * r0) || (r <= P.bnec * r0 && r > rlast);
+        }
+        // ---- restart test (cuPDLP+-style: sufficient decay / necessary decay without
+        // progress / artificial: the Halpern run is a fixed fraction of the solve)
+        const bool restart = (r <= P.bsuff * r0) || (r <= P.bnec * r0 && r > rlast) ||
+                             (it > 0 && hk >= P.bart * it);
         rlast = r;
         if (restart) {
             double ddx = 0.0, ddy = 0.0;
@@ -526,7 +532,7 @@ k_expect_partial(phgpu_state st, const double* __restrict__ obj, const double* _
         v[0] = p * obj[s];
         v[1] = p * bound[s];
         v[2] = p;
-        v[3] = status[s] == PHGPU_OPTIMAL ? p : 0.0;
+        v[3] = (status[s] == PHGPU_OPTIMAL || status[s] == PHGPU_ITER_LIMIT) ? p : 0.0;
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -580,7 +586,8 @@ extern "C" int phgpu_default_options(phgpu_options* o) {
     o->eta_frac = 0.998;
     o->omega0 = 1.0;
     o->keep_omega = 1;
-    o->reserved = 0;
+    o->restart_every = 16;
+    o->beta_artificial = 0.36;
     return 0;
 }
 
@@ -780,15 +787,17 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     if (opt) o = *opt;
     else phgpu_default_options(&o);
     if (o.check_every < 1 || o.max_iter < 1 || !(o.eta_frac > 0.0 && o.eta_frac < 1.0) ||
-        o.gamma < 0.0 || o.gamma > 1.0)
-        return set_err(-1, "bad options (check_every=%d max_iter=%d eta_frac=%g gamma=%g)",
-                       o.check_every, o.max_iter, o.eta_frac, o.gamma);
+        o.gamma < 0.0 || o.gamma > 1.0 || o.restart_every < 1 || o.check_every % o.restart_every != 0)
+        return set_err(-1, "bad options (check_every=%d restart_every=%d max_iter=%d eta_frac=%g gamma=%g)",
+                       o.check_every, o.restart_every, o.max_iter, o.eta_frac, o.gamma);
     solve_params P;
     P.eps_rel = o.eps_rel;
     P.eps_abs = o.eps_abs;
     P.gamma = o.gamma;
     P.bsuff = o.beta_sufficient;
     P.bnec = o.beta_necessary;
+    P.bart = o.beta_artificial > 0.0 ? o.beta_artificial : 1e300;
+    P.restart_every = o.restart_every;
     P.eta_frac = o.eta_frac;
     P.omega0 = o.omega0;
     P.max_iter = o.max_iter;

@@ -30,7 +30,8 @@ class PhgpuOptions(ctypes.Structure):
         ("eta_frac", c_dbl),
         ("omega0", c_dbl),
         ("keep_omega", c_i32),
-        ("reserved", c_i32),
+        ("restart_every", c_i32),
+        ("beta_artificial", c_dbl),
     ]
 
 

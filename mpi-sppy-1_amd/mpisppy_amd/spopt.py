@@ -70,9 +70,13 @@ class SPOpt(SPBase):
                   % (self.solve_times[-1], *self.pdhg_iters[-1]))
         if gripe:
             st = self.engine.status.cpu().numpy()
-            bad = np.nonzero(st != _lib.OPTIMAL)[0]
+            bad = np.nonzero((st != _lib.OPTIMAL) & (st != _lib.ITER_LIMIT))[0]
             for k in bad[:10]:
                 print(f"Solve failed for scenario {self.batch.names[k]} (status {st[k]})")
+            lim = np.nonzero(st == _lib.ITER_LIMIT)[0]
+            if len(lim) and self.cylinder_rank == 0:
+                print(f"WARNING: {len(lim)} scenario(s) hit the PDHG iteration limit "
+                      f"(e.g. {self.batch.names[lim[0]]}); their solutions are approximate")
 
     # spopt.py:310-343 ("weighted, proxed" objective, phbase.py:991)
     def Eobjective(self, verbose=False):

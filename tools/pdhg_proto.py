@@ -68,7 +68,7 @@ class Proto:
         self.y = np.zeros((S, m))
 
     def solve(self, c, q, eps=1e-9, max_iter=100000, gamma=1.0, check=64, warm=True,
-              eta_frac=0.998, verbose=False, omega0=None):
+              eta_frac=0.998, verbose=False, omega0=None, restart_every=None, theta=0.5, art=None):
         b = self.b
         S, n, m = b.S, b.n, b.m
         rp, ci, A, Dr, Dc = b.row_ptr, b.col_idx, self.Ah, self.Dr, self.Dc
@@ -116,6 +116,31 @@ class Proto:
         restarts = np.zeros(S, int)
         while total < max_iter:
             xt, yt, atyt = T(x, y, aty)
+            re_ = restart_every or check
+            if total % re_ == 0 and total % check != 0:
+                r = wnorm(x - xt, y - yt)
+                if r0 is None:
+                    r0 = r.copy(); rlast = r.copy()
+                rs = (r <= 0.2 * r0) | ((r <= 0.8 * r0) & (r > rlast))
+                if art is not None:
+                    rs |= k >= art * np.maximum(total, 1)
+                rs &= ~done
+                if rs.any():
+                    dx = np.linalg.norm(xt - x0, axis=1)
+                    dy = np.linalg.norm(yt - y0, axis=1)
+                    upd = rs & (dx > 1e-10) & (dy > 1e-10)
+                    lw = np.log(omega[:, 0])
+                    lw[upd] = theta * np.log(dy[upd] / dx[upd]) + (1 - theta) * lw[upd]
+                    omega = np.exp(lw)[:, None]
+                    x0[rs], y0[rs], aty0[rs] = xt[rs], yt[rs], atyt[rs]
+                    x[rs], y[rs], aty[rs] = xt[rs], yt[rs], atyt[rs]
+                    k[rs] = 0
+                    r0[rs] = wnorm(x - T(x, y, aty)[0], y - T(x, y, aty)[1])[rs]
+                    restarts[rs] += 1
+                    rlast = r
+                    total += 1
+                    continue
+                rlast = r
             if total % check == 0:
                 r = wnorm(x - xt, y - yt)
                 if r0 is None:
@@ -132,14 +157,16 @@ class Proto:
                     x, y = xt, yt
                     break
                 # restarts
-                rs = (r <= 0.2 * r0) | ((r <= 0.8 * r0) & (r > rlast)) | (k >= 0.36 * max(total, 1) * 0 + 1e18)
+                rs = (r <= 0.2 * r0) | ((r <= 0.8 * r0) & (r > rlast))
+                if art is not None:
+                    rs |= k >= art * np.maximum(total, 1)
                 rs &= ~done
                 if rs.any():
                     dx = np.linalg.norm(xt - x0, axis=1)
                     dy = np.linalg.norm(yt - y0, axis=1)
                     upd = rs & (dx > 1e-10) & (dy > 1e-10)
                     lw = np.log(omega[:, 0])
-                    lw[upd] = 0.5 * np.log(dy[upd] / dx[upd]) + 0.5 * lw[upd]
+                    lw[upd] = theta * np.log(dy[upd] / dx[upd]) + (1 - theta) * lw[upd]
                     omega = np.exp(lw)[:, None]
                     x0[rs], y0[rs], aty0[rs] = xt[rs], yt[rs], atyt[rs]
                     x[rs], y[rs], aty[rs] = xt[rs], yt[rs], atyt[rs]
