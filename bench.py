@@ -33,7 +33,7 @@ def parse():
     p.add_argument("--scens", type=int, default=65536)
     p.add_argument("--cm", type=int, default=1)
     p.add_argument("--rho", type=float, default=1.0)
-    p.add_argument("--eps", type=float, default=1e-10)
+    p.add_argument("--eps", type=float, default=1e-9)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     return p.parse_args()

@@ -58,7 +58,7 @@ enum {
 /* Solver options (the iter0_solver_options / iterk_solver_options dicts of
  * phbase.py:273-274 become these fields). */
 typedef struct {
-    double eps_rel;        /* relative KKT tolerance (primal, dual, gap)      [1e-10] */
+    double eps_rel;        /* relative KKT tolerance (primal, dual, gap)      [1e-9] */
     double eps_abs;        /* absolute KKT tolerance                          [1e-12] */
     int32_t max_iter;      /* PDHG iteration cap per scenario                 [100000] */
     int32_t check_every;   /* KKT / restart check period (iterations)         [64] */
@@ -71,6 +71,7 @@ typedef struct {
     int32_t restart_every; /* restart test period (iterations; divides check_every) [16] */
     double beta_artificial;/* restart when the Halpern run exceeds this fraction
                               of all iterations of the solve                  [0.36] */
+    double omega_clamp;    /* primal weight kept in [1/clamp, clamp] (scaled) [1e4] */
 } phgpu_options;
 
 /* Fill *opt with the defaults shown above. */

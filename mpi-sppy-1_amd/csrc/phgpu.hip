@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
 
 // ------------------------------------------------------------------ solve kernel
 struct solve_params {
-    double eps_rel, eps_abs, gamma, bsuff, bnec, bart, eta_frac, omega0;
+    double eps_rel, eps_abs, gamma, bsuff, bnec, bart, eta_frac, omega0, wmin, wmax;
     int max_iter, check_every, restart_every, warm, keep_omega;
 };
 
@@ -390,7 +390,8 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             }
             ddx = sqrt(ddx);
             ddy = sqrt(ddy);
-            if (ddx > 1e-10 && ddy > 1e-10) omega = exp(0.5 * log(ddy / ddx) + 0.5 * log(omega));
+            if (ddx > 1e-10 && ddy > 1e-10)
+                omega = clampd(exp(0.5 * log(ddy / ddx) + 0.5 * log(omega)), P.wmin, P.wmax);
             hk = 0;
             r0 = -1.0;
             rlast = INFINITY;
@@ -468,21 +469,37 @@ k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict_
     }
 }
 
-// One thread per nonant: ordered run-sum over the waves' partials.
-__global__ void k_xbar_final(phgpu_state st, double* __restrict__ node_buf) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= st.nn) return;
+// Ordered segmented sum of the per-wave partials, one block per nonant.  The local
+// scenarios are in tree order, so each node's waves form ONE contiguous run: a run
+// that lies inside one thread's chunk of waves is complete and is flushed directly;
+// the first / last run of every chunk go through shared memory and thread 0 merges
+// them in chunk order (deterministic for every wave-uniform node).
+#define XF_THREADS 256
+__global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, double* __restrict__ node_buf) {
+    __shared__ int fnode[XF_THREADS], lnode[XF_THREADS];
+    __shared__ double fa[XF_THREADS], fb[XF_THREADS], la[XF_THREADS], lb[XF_THREADS];
+    const int k = blockIdx.x;
+    const int t = threadIdx.x;
     const int half = st.num_nodes * st.nlen_max;
     const int off = st.nonant_off[k];
-    int cur = -1;
-    double a = 0.0, b = 0.0;
-    for (int64_t w = 0; w < st.nwaves; ++w) {
+    const int64_t nw = st.nwaves;
+    const int64_t C = (nw + XF_THREADS - 1) / XF_THREADS;
+    const int64_t w0 = (int64_t)t * C, w1 = (w0 + C < nw) ? w0 + C : nw;
+    int cur = -1, first = -1;
+    double a = 0.0, b = 0.0, a_first = 0.0, b_first = 0.0;
+    for (int64_t w = w0; w < w1; ++w) {
         const int gnode = st.part_node[w * st.nn + k];
         if (gnode < 0) continue;
         if (gnode != cur) {
             if (cur >= 0) {
-                node_buf[cur * st.nlen_max + off] += a;
-                node_buf[half + cur * st.nlen_max + off] += b;
+                if (first < 0) {  // close the chunk's first run
+                    first = cur;
+                    a_first = a;
+                    b_first = b;
+                } else {          // a complete middle run
+                    atomicAdd(&node_buf[cur * st.nlen_max + off], a);
+                    atomicAdd(&node_buf[half + cur * st.nlen_max + off], b);
+                }
             }
             cur = gnode;
             a = 0.0;
@@ -491,9 +508,45 @@ __global__ void k_xbar_final(phgpu_state st, double* __restrict__ node_buf) {
         a += st.part[(w * st.nn + k) * 2 + 0];
         b += st.part[(w * st.nn + k) * 2 + 1];
     }
-    if (cur >= 0) {
-        node_buf[cur * st.nlen_max + off] += a;
-        node_buf[half + cur * st.nlen_max + off] += b;
+    if (first < 0) {  // zero or one run in this chunk: it is the first (and last) run
+        fnode[t] = cur;
+        fa[t] = a;
+        fb[t] = b;
+        lnode[t] = -1;
+        la[t] = lb[t] = 0.0;
+    } else {
+        fnode[t] = first;
+        fa[t] = a_first;
+        fb[t] = b_first;
+        lnode[t] = cur;
+        la[t] = a;
+        lb[t] = b;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int c = -1;
+        double sa = 0.0, sb = 0.0;
+        for (int u = 0; u < XF_THREADS; ++u) {
+            for (int side = 0; side < 2; ++side) {
+                const int g = side ? lnode[u] : fnode[u];
+                if (g < 0) continue;
+                if (g != c) {
+                    if (c >= 0) {
+                        node_buf[c * st.nlen_max + off] += sa;
+                        node_buf[half + c * st.nlen_max + off] += sb;
+                    }
+                    c = g;
+                    sa = 0.0;
+                    sb = 0.0;
+                }
+                sa += side ? la[u] : fa[u];
+                sb += side ? lb[u] : fb[u];
+            }
+        }
+        if (c >= 0) {
+            node_buf[c * st.nlen_max + off] += sa;
+            node_buf[half + c * st.nlen_max + off] += sb;
+        }
     }
 }
 
@@ -576,7 +629,7 @@ static int dalloc(phgpu_state* h, T** p, size_t count) {
 
 extern "C" int phgpu_default_options(phgpu_options* o) {
     if (!o) return set_err(-1, "null options");
-    o->eps_rel = 1e-10;
+    o->eps_rel = 1e-9;
     o->eps_abs = 1e-12;
     o->max_iter = 100000;
     o->check_every = 64;
@@ -588,6 +641,7 @@ extern "C" int phgpu_default_options(phgpu_options* o) {
     o->keep_omega = 1;
     o->restart_every = 16;
     o->beta_artificial = 0.36;
+    o->omega_clamp = 1e4;
     return 0;
 }
 
@@ -798,6 +852,8 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     P.bnec = o.beta_necessary;
     P.bart = o.beta_artificial > 0.0 ? o.beta_artificial : 1e300;
     P.restart_every = o.restart_every;
+    P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
+    P.wmin = 1.0 / P.wmax;
     P.eta_frac = o.eta_frac;
     P.omega0 = o.omega0;
     P.max_iter = o.max_iter;
@@ -819,7 +875,7 @@ extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf
     if (h->nn == 0) return 0;
     hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_xbar_final, dim3((h->nn + 63) / 64), dim3(64), 0, st, *h, node_buf);
+    hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf);
     HIPCHK(hipGetLastError());
     return 0;
 }

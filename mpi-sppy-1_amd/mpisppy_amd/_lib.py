@@ -32,6 +32,7 @@ class PhgpuOptions(ctypes.Structure):
         ("keep_omega", c_i32),
         ("restart_every", c_i32),
         ("beta_artificial", c_dbl),
+        ("omega_clamp", c_dbl),
     ]
 
 

@@ -48,8 +48,8 @@ def test_nm_shows_extern_c(lib):
 def test_host_only_calls(lib):
     """Calls that touch no device: default options, last_error, null-handle errors."""
     from mpisppy_amd import _lib
-    o = _lib.default_options(eps_rel=1e-9)
-    assert o.eps_rel == 1e-9 and o.check_every == 64 and o.max_iter == 100000
+    o = _lib.default_options(eps_abs=1e-13)
+    assert o.eps_rel == 1e-9 and o.omega_clamp == 1e4 and o.check_every == 64 and o.max_iter == 100000
     L = _lib.load()
     assert L.phgpu_destroy(None) == 0
     assert L.phgpu_set_ph_state(None, None, None, None, 0, 0) != 0

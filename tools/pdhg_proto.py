@@ -68,7 +68,7 @@ class Proto:
         self.y = np.zeros((S, m))
 
     def solve(self, c, q, eps=1e-9, max_iter=100000, gamma=1.0, check=64, warm=True,
-              eta_frac=0.998, verbose=False, omega0=None, restart_every=None, theta=0.5, art=None):
+              eta_frac=0.998, verbose=False, omega0=None, restart_every=None, theta=0.5, art=None, kernel_mode=False, km_hk0=True, km_rlast_inf=True, trace=None, wclamp=None):
         b = self.b
         S, n, m = b.S, b.n, b.m
         rp, ci, A, Dr, Dc = b.row_ptr, b.col_idx, self.Ah, self.Dr, self.Dc
@@ -131,6 +131,8 @@ class Proto:
                     upd = rs & (dx > 1e-10) & (dy > 1e-10)
                     lw = np.log(omega[:, 0])
                     lw[upd] = theta * np.log(dy[upd] / dx[upd]) + (1 - theta) * lw[upd]
+                    if wclamp is not None:
+                        lw = np.clip(lw, -np.log(wclamp), np.log(wclamp))
                     omega = np.exp(lw)[:, None]
                     x0[rs], y0[rs], aty0[rs] = xt[rs], yt[rs], atyt[rs]
                     x[rs], y[rs], aty[rs] = xt[rs], yt[rs], atyt[rs]
@@ -138,6 +140,10 @@ class Proto:
                     r0[rs] = wnorm(x - T(x, y, aty)[0], y - T(x, y, aty)[1])[rs]
                     restarts[rs] += 1
                     rlast = r
+                    if kernel_mode and km_rlast_inf:
+                        rlast = np.where(rs, np.inf, r)
+                    if kernel_mode and not km_hk0:
+                        k[rs] = 1
                     total += 1
                     continue
                 rlast = r
@@ -150,6 +156,9 @@ class Proto:
                 xo = xt * Dc
                 yo = yt * Dr
                 conv = self._kkt(xo, yo, c, q, eps)
+                if trace is not None:
+                    t_ = trace['idx']
+                    trace.setdefault('rows', []).append((total, float(omega[t_, 0]), float(r[t_]), float(r0[t_]), int(k[t_]), float(self.last_pobj[t_]), float(self.last_dobj[t_]), int(restarts[t_])))
                 newly = conv & ~done
                 iters[newly] = total
                 done |= conv
@@ -167,6 +176,8 @@ class Proto:
                     upd = rs & (dx > 1e-10) & (dy > 1e-10)
                     lw = np.log(omega[:, 0])
                     lw[upd] = theta * np.log(dy[upd] / dx[upd]) + (1 - theta) * lw[upd]
+                    if wclamp is not None:
+                        lw = np.clip(lw, -np.log(wclamp), np.log(wclamp))
                     omega = np.exp(lw)[:, None]
                     x0[rs], y0[rs], aty0[rs] = xt[rs], yt[rs], atyt[rs]
                     x[rs], y[rs], aty[rs] = xt[rs], yt[rs], atyt[rs]
@@ -174,6 +185,12 @@ class Proto:
                     r0[rs] = wnorm(x - T(x, y, aty)[0], y - T(x, y, aty)[1])[rs]
                     restarts[rs] += 1
                 rlast = r
+                if kernel_mode and rs.any():
+                    if km_rlast_inf:
+                        rlast[rs] = np.inf
+                    if km_hk0:
+                        total += 1
+                        continue
             # Halpern step for active scenarios
             kk = k[:, None]
             a1 = (kk + 1) / (kk + 2)
