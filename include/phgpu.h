@@ -72,6 +72,9 @@ typedef struct {
     double beta_artificial;/* restart when the Halpern run exceeds this fraction
                               of all iterations of the solve                  [0.36] */
     double omega_clamp;    /* primal weight kept in [1/clamp, clamp] (scaled) [1e4] */
+    int32_t kernel;        /* 0 auto, 1 global-memory kernel, 2 register-resident
+                              kernel (error if no compiled instance fits)      [0] */
+    int32_t reserved;
 } phgpu_options;
 
 /* Fill *opt with the defaults shown above. */
@@ -158,6 +161,12 @@ int phgpu_last_error(char* buf, size_t len);
 
 /* Workspace bytes held by the handle (diagnostics / memory planning). */
 int64_t phgpu_workspace_bytes(phgpu_handle h);
+
+/* Solve-kernel selection of the handle (diagnostics): info[10] =
+ * {register instance or -1, lanes per scenario L, column slots / CSC entries per
+ *  column / row slots / CSR entries per row actually needed, and the instance's
+ *  compiled bounds KC, ZC, KR, ZR}. */
+int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
 #ifdef __cplusplus
 }

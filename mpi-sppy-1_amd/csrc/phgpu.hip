@@ -20,6 +20,7 @@
 #include <stdarg.h>
 #include <string.h>
 #include <new>
+#include <stdlib.h>
 
 #include "phgpu.h"
 
@@ -68,6 +69,10 @@ struct phgpu_state {
     int32_t* part_node; // [nwaves * nn]
     int64_t nwaves;
     int64_t ws_bytes;
+    // register-resident path (solve_reg.inc): lane plan, -1 instance = unavailable
+    int reg_inst;
+    int reg_L, reg_kc, reg_zc, reg_kr, reg_zr;
+    int32_t *pl_col_k, *pl_col_r, *pl_row_k, *pl_row_c;
     // PH state (caller-owned)
     const double *W, *rho, *xbar;
     int W_on, prox_on;
@@ -167,7 +172,7 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
         st.y[IX(i)] = 0.0;
     }
     // power iteration on A^T A (v in xe, A v in yt, A^T A v in xt)
-    for (int j = 0; j < n; ++j) st.xe[IX(j)] = 1.0;
+    for (int j = 0; j < n; ++j) st.xe[IX(j)] = 1.0 + 0.5 * sin(1.7 * j);
     double lam = 0.0;
     for (int it = 0; it < power_iters; ++it) {
         for (int i = 0; i < m; ++i) {
@@ -189,7 +194,10 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
         const double inv = nv > 0.0 ? 1.0 / nv : 0.0;
         for (int j = 0; j < n; ++j) st.xe[IX(j)] = st.xt[IX(j)] * inv;
     }
-    st.normA[s] = lam > 0.0 ? sqrt(lam) : 1.0;
+    // power iteration under-estimates ||A||_2 (slowly when the top singular values are
+    // close); 1% margin keeps tau * sigma * ||A||^2 < 1 (a violated step condition makes
+    // the reflected Halpern iteration diverge)
+    st.normA[s] = lam > 0.0 ? 1.01 * sqrt(lam) : 1.0;
     st.omega[s] = 1.0;
 }
 
@@ -285,15 +293,17 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     for (; it < P.max_iter; ++it) {
         const double tau = eta / omega, sig = eta * omega;
         const bool kkt = (it % P.check_every) == 0;
-        // non-fused iteration (T(z) kept in xt / yt / xe) at restart-test points
-        const bool check = kkt || (it % P.restart_every) == 0;
+        // non-fused iteration (T(z) kept in xt / yt / xe) at restart-test points and on
+        // the last iteration (the iteration-limit answer is T(z), which is box-feasible)
+        const bool check = kkt || (it % P.restart_every) == 0 || it == P.max_iter - 1;
         const double a1 = (hk + 1.0) / (hk + 2.0), a0 = 1.0 / (hk + 2.0);
         double dx2 = 0.0, dy2 = 0.0;
         // --- primal step: xt = prox(x - tau (c - A^T y)); xe = 2 xt - x
         for (int j = 0; j < n; ++j) {
             const double xj = x[IX(j)];
-            const double xtj = clampd((xj - tau * (ch[IX(j)] - aty[IX(j)])) / (1.0 + tau * qh[IX(j)]),
-                                      st.lbh[IX(j)], st.ubh[IX(j)]);
+            const double qj = qh[IX(j)];
+            const double num = xj - tau * (ch[IX(j)] - aty[IX(j)]);
+            const double xtj = clampd(qj != 0.0 ? num / (1.0 + tau * qj) : num, st.lbh[IX(j)], st.ubh[IX(j)]);
             xe[IX(j)] = 2.0 * xtj - xj;
             const double d = xj - xtj;
             dx2 += d * d;
@@ -410,7 +420,12 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
         for (int j = 0; j < n; ++j) x[IX(j)] = xt[IX(j)];
         for (int i = 0; i < m; ++i) y[IX(i)] = yt[IX(i)];
     } else {
-        // objective / bound at the current iterate
+        // iteration limit: answer T(z) of the last iteration (xt, yt, A^T yt in xe)
+        for (int j = 0; j < n; ++j) {
+            x[IX(j)] = xt[IX(j)];
+            aty[IX(j)] = xe[IX(j)];
+        }
+        for (int i = 0; i < m; ++i) y[IX(i)] = yt[IX(i)];
         pobj = const_term;
         dobj = const_term;
         for (int i = 0; i < m; ++i) dobj += row_dual_term(y[IX(i)] * st.Dr[IX(i)], st.rl[IX(i)], st.ru[IX(i)]);
@@ -431,6 +446,8 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     status[s] = stat;
     if (iters) iters[s] = final_is_t ? it : P.max_iter;
 }
+
+#include "solve_reg.inc"
 
 // ------------------------------------------------------------------ PH reductions
 // phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
@@ -610,6 +627,72 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__
     if (threadIdx.x == 0) out[k] = sh[0] * scale;
 }
 
+// ------------------------------------------------------------------ lane plan (host)
+#include <vector>
+#include <algorithm>
+
+// Build the per-lane plan of solve_reg.inc for L lanes per scenario: lane l owns
+// columns j = l + q L and rows i = l + r L; each column's CSC entries and each row's
+// CSR entries are padded to the instance's ZC / ZR slots.  Returns false if no
+// compiled instance fits (then the global-memory kernel is used).
+static bool build_plan(int L, int n, int m, const int32_t* row_ptr, const int32_t* col_idx,
+                       int* inst_out, int* kc_out, int* zc_out, int* kr_out, int* zr_out,
+                       std::vector<int32_t>& col_k, std::vector<int32_t>& col_r,
+                       std::vector<int32_t>& row_k, std::vector<int32_t>& row_c) {
+    if (m < 1 || n < 1) return false;
+    const int kc = (n + L - 1) / L;
+    const int kr = (m + L - 1) / L;
+    std::vector<std::vector<std::pair<int, int>>> cols(n);  // (csr k, row)
+    for (int i = 0; i < m; ++i)
+        for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) cols[col_idx[k]].push_back({k, i});
+    int zc = 1, zr = 1;
+    for (int j = 0; j < n; ++j) zc = std::max(zc, (int)cols[j].size());
+    for (int i = 0; i < m; ++i) zr = std::max(zr, (int)(row_ptr[i + 1] - row_ptr[i]));
+    int inst = -1;
+    long best = 0;
+    const int ninst = (int)(sizeof(g_reg_instances) / sizeof(g_reg_instances[0]));
+    for (int a = 0; a < ninst; ++a) {
+        const reg_instance& r = g_reg_instances[a];
+        if (r.KC >= kc && r.ZC >= zc && r.KR >= kr && r.ZR >= zr) {
+            // register-cost estimate in doubles per lane
+            const long cost = (long)r.KC * (13 + r.ZC) + (long)r.KR * (7 + r.ZR);
+            if (inst < 0 || cost < best) {
+                inst = a;
+                best = cost;
+            }
+        }
+    }
+    if (inst < 0) return false;
+    col_k.assign((size_t)L * kc * zc, -1);
+    col_r.assign((size_t)L * kc * zc, 0);
+    for (int u = 0; u < L; ++u)
+        for (int q = 0; q < kc; ++q) {
+            const int j = u + q * L;
+            if (j >= n) continue;
+            for (int z = 0; z < (int)cols[j].size(); ++z) {
+                col_k[((size_t)u * kc + q) * zc + z] = cols[j][z].first;
+                col_r[((size_t)u * kc + q) * zc + z] = cols[j][z].second;
+            }
+        }
+    row_k.assign((size_t)L * kr * zr, -1);
+    row_c.assign((size_t)L * kr * zr, 0);
+    for (int u = 0; u < L; ++u)
+        for (int r = 0; r < kr; ++r) {
+            const int i = u + r * L;
+            if (i >= m) continue;
+            for (int k = row_ptr[i], z = 0; k < row_ptr[i + 1]; ++k, ++z) {
+                row_k[((size_t)u * kr + r) * zr + z] = k;
+                row_c[((size_t)u * kr + r) * zr + z] = col_idx[k];
+            }
+        }
+    *inst_out = inst;
+    *kc_out = kc;
+    *zc_out = zc;
+    *kr_out = kr;
+    *zr_out = zr;
+    return true;
+}
+
 // ------------------------------------------------------------------ C-ABI
 template <typename T>
 static int dalloc(phgpu_state* h, T** p, size_t count) {
@@ -642,6 +725,7 @@ extern "C" int phgpu_default_options(phgpu_options* o) {
     o->restart_every = 16;
     o->beta_artificial = 0.36;
     o->omega_clamp = 1e4;
+    o->kernel = 0;
     return 0;
 }
 
@@ -780,6 +864,56 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
         phgpu_destroy(h);
         return set_err(-2, "pattern upload failed: %s", hipGetErrorString(e));
     }
+    // register-resident path: lanes per scenario L (power of two <= 64).  Smallest L
+    // with a fitting instance, doubled while the grid has fewer than 4 lanes per
+    // (SIMD lane x wave slot) of the chip and a scenario still has columns to spread.
+    h->reg_inst = -1;
+    {
+        // lanes per scenario: the smallest L with a fitting instance, doubled while the
+        // grid holds fewer than 4 waves per SIMD of the chip and a scenario still has
+        // columns to spread; PHGPU_LANES=<L> pins it (tuning / tests)
+        const int64_t target = (int64_t)256 * 4 * WAVE * 4;
+        const char* env = getenv("PHGPU_LANES");
+        const int pinned = env ? atoi(env) : 0;
+        int chosen = -1;
+        std::vector<int32_t> ck, cr, rk, rc;
+        int inst = -1, kc = 0, zc = 0, kr = 0, zr = 0;
+        for (int L = 1; L <= WAVE; L *= 2) {
+            if (pinned > 0 && L != pinned) continue;
+            std::vector<int32_t> a1, a2, a3, a4;
+            int i1, i2, i3, i4, i5;
+            if (!build_plan(L, n, m, row_ptr, col_idx, &i1, &i2, &i3, &i4, &i5, a1, a2, a3, a4)) continue;
+            if (pinned <= 0 && chosen >= 0 && (S * (int64_t)chosen >= target || chosen >= n)) break;
+            chosen = L;
+            inst = i1; kc = i2; zc = i3; kr = i4; zr = i5;
+            ck.swap(a1); cr.swap(a2); rk.swap(a3); rc.swap(a4);
+        }
+        if (chosen > 0) {
+            int rc2 = 0;
+            rc2 |= dalloc(h, &h->pl_col_k, ck.size());
+            rc2 |= dalloc(h, &h->pl_col_r, cr.size());
+            rc2 |= dalloc(h, &h->pl_row_k, rk.size());
+            rc2 |= dalloc(h, &h->pl_row_c, rc.size());
+            if (rc2) {
+                phgpu_destroy(h);
+                return set_err(-3, "plan allocation failed");
+            }
+            e = hipMemcpy(h->pl_col_k, ck.data(), ck.size() * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(h->pl_col_r, cr.data(), cr.size() * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(h->pl_row_k, rk.data(), rk.size() * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(h->pl_row_c, rc.data(), rc.size() * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                phgpu_destroy(h);
+                return set_err(-2, "plan upload failed: %s", hipGetErrorString(e));
+            }
+            h->reg_inst = inst;
+            h->reg_L = chosen;
+            h->reg_kc = kc;
+            h->reg_zc = zc;
+            h->reg_kr = kr;
+            h->reg_zr = zr;
+        }
+    }
     *out = h;
     return 0;
 }
@@ -813,7 +947,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     HIPCHK(cp(h->prob, prob, Sz));
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_setup, grid_for(h->S), dim3(BLOCK), 0, st, *h, 10, 40);
+    hipLaunchKernelGGL(k_setup, grid_for(h->S), dim3(BLOCK), 0, st, *h, 10, 200);
     HIPCHK(hipGetLastError());
     h->have_solution = 0;
     return 0;
@@ -852,16 +986,37 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     P.bnec = o.beta_necessary;
     P.bart = o.beta_artificial > 0.0 ? o.beta_artificial : 1e300;
     P.restart_every = o.restart_every;
-    P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
-    P.wmin = 1.0 / P.wmax;
     P.eta_frac = o.eta_frac;
     P.omega0 = o.omega0;
     P.max_iter = o.max_iter;
     P.check_every = o.check_every;
     P.warm = (warm_start && h->have_solution) ? 1 : 0;
     P.keep_omega = o.keep_omega;
+    P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
+    P.wmin = 1.0 / P.wmax;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+    const bool use_reg = (o.kernel == 2) || (o.kernel == 0 && h->reg_inst >= 0);
+    if (o.kernel == 2 && h->reg_inst < 0)
+        return set_err(-1, "register-resident kernel requested but no compiled instance fits this pattern");
+    if (use_reg) {
+        reg_plan pl;
+        pl.L = h->reg_L;
+        pl.kc = h->reg_kc;
+        pl.zc = h->reg_zc;
+        pl.kr = h->reg_kr;
+        pl.zr = h->reg_zr;
+        pl.col_k = h->pl_col_k;
+        pl.col_r = h->pl_col_r;
+        pl.row_k = h->pl_row_k;
+        pl.row_c = h->pl_row_c;
+        const int G = WAVE / pl.L;
+        const size_t lds = (size_t)G * (size_t)(h->n + h->m + 2) * sizeof(double);
+        const dim3 grid((unsigned)((h->S + G - 1) / G));
+        hipLaunchKernelGGL(g_reg_instances[h->reg_inst].fn, grid, dim3(WAVE), lds, st, *h, P, pl, x, y, obj,
+                           bound, status, iters);
+    } else {
+        hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+    }
     HIPCHK(hipGetLastError());
     h->have_solution = 1;
     return 0;
@@ -915,7 +1070,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->A, h->c, h->lb, h->ub, h->q, h->rl, h->ru, h->objc, h->prob, h->pcoef,
                     h->node_of, h->Ah_csr, h->Ah_csc, h->Dr, h->Dc, h->normA, h->lbh, h->ubh,
                     h->rlh, h->ruh, h->ch, h->qh, h->x, h->x0, h->xe, h->xt, h->aty, h->aty0,
-                    h->y, h->y0, h->yt, h->omega, h->part, h->part_node};
+                    h->y, h->y0, h->yt, h->omega, h->part, h->part_node, h->pl_col_k,
+                    h->pl_col_r, h->pl_row_k, h->pl_row_c};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -930,3 +1086,23 @@ extern "C" int phgpu_last_error(char* buf, size_t len) {
 }
 
 extern "C" int64_t phgpu_workspace_bytes(phgpu_handle h) { return h ? h->ws_bytes : -1; }
+
+extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
+    if (!h || !info) return set_err(-1, "null argument");
+    info[0] = h->reg_inst;
+    info[1] = h->reg_L;
+    info[2] = h->reg_kc;
+    info[3] = h->reg_zc;
+    info[4] = h->reg_kr;
+    info[5] = h->reg_zr;
+    if (h->reg_inst >= 0) {
+        const reg_instance& r = g_reg_instances[h->reg_inst];
+        info[6] = r.KC;
+        info[7] = r.ZC;
+        info[8] = r.KR;
+        info[9] = r.ZR;
+    } else {
+        info[6] = info[7] = info[8] = info[9] = 0;
+    }
+    return 0;
+}

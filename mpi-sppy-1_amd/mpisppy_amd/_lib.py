@@ -33,6 +33,8 @@ class PhgpuOptions(ctypes.Structure):
         ("restart_every", c_i32),
         ("beta_artificial", c_dbl),
         ("omega_clamp", c_dbl),
+        ("kernel", c_i32),
+        ("reserved", c_i32),
     ]
 
 
@@ -41,7 +43,7 @@ OPTIMAL, ITER_LIMIT, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE = 0, 1, 2, 3
 # every symbol include/phgpu.h declares (tests check the library exports them all)
 EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_set_scenarios", "phgpu_set_ph_state",
            "phgpu_solve", "phgpu_ph_reduce", "phgpu_ph_update", "phgpu_expectations",
-           "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes"]
+           "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes", "phgpu_kernel_info"]
 
 _lib = None
 
@@ -74,6 +76,7 @@ def load(path=None):
     lib.phgpu_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     lib.phgpu_workspace_bytes.argtypes = [c_vp]
     lib.phgpu_workspace_bytes.restype = c_i64
+    lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     for name in EXPORTS:
         if name != "phgpu_workspace_bytes":
             getattr(lib, name).restype = c_int

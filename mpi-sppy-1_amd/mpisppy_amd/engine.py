@@ -130,6 +130,13 @@ class PHEngine:
     def workspace_bytes(self):
         return int(self.lib.phgpu_workspace_bytes(self.h))
 
+    def kernel_info(self):
+        """Which solve kernel the handle uses (phgpu_kernel_info)."""
+        info = (ctypes.c_int32 * 10)()
+        _lib.check(self.lib.phgpu_kernel_info(self.h, info), "phgpu_kernel_info")
+        keys = ["instance", "lanes", "kc", "zc", "kr", "zr", "KC", "ZC", "KR", "ZR"]
+        return dict(zip(keys, list(info)))
+
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):
         """rho: scalar or host [S, nn] array (the rho Params of phbase.py:598-602)."""

@@ -62,6 +62,9 @@ def scenario_creator(sname, **kwargs):
         raise RuntimeError("scenario_creator for aircond needs branching_factors in kwargs")
     if _kw(kwargs, "start_ups"):
         raise NotImplementedError("start_ups (binaries) is outside the LP/QP hot path")
+    # parameters the caller leaves out take the module defaults (what kw_creator does
+    # in the reference, aircond.py:19-35 / 441-460)
+    kwargs = {**{k: v for k, v in PARMS.items() if k != "start_seed"}, **kwargs}
     bfs = list(kwargs["branching_factors"])
     demands, nodenames = demands_creator(sname, bfs, **kwargs)
     T = len(demands)
@@ -135,6 +138,7 @@ def batch_creator(scenario_names, **kwargs):
     template scenario; per scenario only the material-balance right-hand sides
     (demands) and tree node ids change."""
     names = list(scenario_names)
+    kwargs = {**{k: v for k, v in PARMS.items() if k != "start_seed"}, **kwargs}
     bfs = list(kwargs["branching_factors"])
     tmpl = scenario_creator(names[0], **kwargs)
     all_nodes = create_nodenames_from_branching_factors(bfs)

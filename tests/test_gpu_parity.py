@@ -233,3 +233,38 @@ def test_capi_errors_are_loud(gpu):
     assert rc != 0 and "row_ptr" in _lib.last_error()
     with pytest.raises(_lib.PhgpuError):
         _lib.check(rc, "phgpu_create")
+
+
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_both_solve_kernels_match_oracle(gpu, kernel):
+    """The global-memory kernel (1) and the register-resident kernel (2) both reproduce
+    the farmer 3-scenario trajectory and agree on random LP batches."""
+    from mpisppy_amd.examples import farmer
+    names = farmer.scenario_names_creator(3)
+    opt = {"kernel": kernel}
+    ph = _ph(names, farmer.scenario_creator, {"num_scens": 3}, iter0_solver_options=opt,
+             iterk_solver_options=opt)
+    conv, eobj, tb = ph.ph_main()
+    g = GOLD["farmer3_rho1"]
+    assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
+    assert np.abs(ph.W_array() - np.array(g["traj"][4]["W"])).max() <= ABS
+
+
+def test_register_kernel_on_random_batches(gpu):
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    for S, wq, seed in [(5, False, 1), (97, True, 2), (300, False, 3)]:
+        b = _random_lp_batch(S, 11, 7, 0.35, seed=seed, with_q=wq)
+        e = PHEngine(b, device="cuda:0")
+        info = e.kernel_info()
+        assert info["instance"] >= 0, info
+        e.solve(_lib.default_options(kernel=1), warm=False)
+        o1 = e.host("obj").copy()
+        b1 = e.host("bound").copy()
+        e.solve(_lib.default_options(kernel=2), warm=False)
+        o2 = e.host("obj")
+        assert (e.host("status") == 0).all()
+        tol = OBJ_REL * np.maximum(1.0, np.abs(o1))
+        assert np.all(np.abs(o1 - o2) <= tol), (o1, o2)
+        assert np.all(np.abs(e.host("bound") - b1) <= tol)
+        e.close()

@@ -58,12 +58,12 @@ class Proto:
             Dc *= cs
         self.Ah, self.Dr, self.Dc, self.rows = A, Dr, Dc, rows
         # power iteration for ||Ah||_2
-        v = np.ones((S, n))
-        for _ in range(40):
+        v = (1 + 0.5 * np.sin(1.7 * np.arange(n)))[None, :].repeat(S, 0)
+        for _ in range(200):
             w = spmvT(rp, ci, A, spmv(rp, ci, A, v), n)
             nv = np.linalg.norm(w, axis=1, keepdims=True)
             v = w / np.maximum(nv, 1e-300)
-        self.normA = np.sqrt(np.maximum(nv[:, 0], 1e-300))
+        self.normA = 1.01 * np.sqrt(np.maximum(nv[:, 0], 1e-300))
         self.x = np.zeros((S, n))
         self.y = np.zeros((S, m))
 
