@@ -177,8 +177,23 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=e.device)
     comm.allreduce_max_(t)
     elapsed = float(t.item())
-    # roofline of the dominant kernel (k_solve): algorithmic bytes per launch
+    # roofline of the dominant kernel (the batched solve): algorithmic bytes per launch
     n, m, nnz, nn = b.n, b.m, b.nnz, b.nn
+    kinfo = e.kernel_info()
+    if kinfo["instance"] >= 0:
+        kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}>"
+    else:
+        kname = "k_solve"
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_summary_farmer{a.scens}_cm{a.cm}.json")
+    if world == 1 and os.path.exists(pmc):
+        try:
+            d = json.load(open(pmc))
+            if ("void " + kname) in d["kernels"]:
+                traffic = d["k_solve_reg_traffic_bytes_per_launch"]["total_upper"]
+                traffic_src = os.path.relpath(pmc, ROOT)
+        except Exception:
+            traffic = None
     B = 8 * (nnz + 5 * n + 4 * m + 3 * nn)           # SURVEY.md 8(d), per PDHG iter per scenario
     units = float(it_host.sum())                     # scenario-iterations of the last launch
     solve_s = float(np.mean(solve_ms[-1:])) / 1e3
@@ -209,9 +224,15 @@ def main():
             "trivial_bound": trivial_bound,
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_solve", "bytes_per_scenario_iter": B,
-                         "scenario_iters_per_launch": units, "launch_ms": solve_s * 1e3},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "kernel": kname, "lanes_per_scenario": kinfo["lanes"],
+                         "bytes_per_scenario_iter": B,
+                         "scenario_iters_per_launch": units, "launch_ms": solve_s * 1e3,
+                         "note": ("achieved = algorithmic PDHG bytes (SURVEY.md 8(d): 8*(nnz+5n+4m+3nn) per "
+                                  "scenario-iteration) / launch time; the register-resident kernel keeps the "
+                                  "iterates in VGPRs/LDS, so measured HBM traffic per launch (PMC FETCH_SIZE*2 + "
+                                  "WRITE_SIZE) is far below it")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
