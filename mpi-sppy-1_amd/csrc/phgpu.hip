@@ -73,6 +73,8 @@ struct phgpu_state {
     int reg_inst;
     int reg_L, reg_kc, reg_zc, reg_kr, reg_zr;
     int32_t *pl_col_k, *pl_col_r, *pl_row_k, *pl_row_c;
+    int* qhead;  // work-queue head of the persistent solve kernel
+    int num_cus;
     // PH state (caller-owned)
     const double *W, *rho, *xbar;
     int W_on, prox_on;
@@ -838,6 +840,13 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
     ALLOC(h->y0, (size_t)m * Sz);
     ALLOC(h->yt, (size_t)m * Sz);
     ALLOC(h->omega, Sz);
+    ALLOC(h->qhead, 1);
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
+            ncu = 256;
+        h->num_cus = ncu;
+    }
     {
         size_t K = (size_t)(2 * nn > 4 ? 2 * nn : 4);
         ALLOC(h->part, (size_t)h->nwaves * K);
@@ -870,9 +879,9 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
     h->reg_inst = -1;
     {
         // lanes per scenario: the smallest L with a fitting instance, doubled while the
-        // grid holds fewer than 4 waves per SIMD of the chip and a scenario still has
+        // grid holds fewer than 8 waves per SIMD of the chip and a scenario still has
         // columns to spread; PHGPU_LANES=<L> pins it (tuning / tests)
-        const int64_t target = (int64_t)256 * 4 * WAVE * 4;
+        const int64_t target = (int64_t)256 * 4 * WAVE * 8;
         const char* env = getenv("PHGPU_LANES");
         const int pinned = env ? atoi(env) : 0;
         int chosen = -1;
@@ -1011,9 +1020,19 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_c = h->pl_row_c;
         const int G = WAVE / pl.L;
         const size_t lds = (size_t)G * (size_t)(h->n + h->m + 2) * sizeof(double);
-        const dim3 grid((unsigned)((h->S + G - 1) / G));
-        hipLaunchKernelGGL(g_reg_instances[h->reg_inst].fn, grid, dim3(WAVE), lds, st, *h, P, pl, x, y, obj,
-                           bound, status, iters);
+        const reg_kernel_t fn = g_reg_instances[h->reg_inst].fn;
+        // persistent grid: co-resident single-wave workgroups (occupancy x CUs), never
+        // more than there are scenario groups
+        int per_cu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, WAVE, lds));
+        if (per_cu < 1) per_cu = 1;
+        const int64_t need = (h->S + G - 1) / G;
+        int64_t nblk = (int64_t)per_cu * h->num_cus;
+        if (nblk > need) nblk = need;
+        const int64_t first_dyn = nblk * G;
+        HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
+        hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE), lds, st, *h, P, pl, h->qhead, first_dyn, x, y,
+                           obj, bound, status, iters);
     } else {
         hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
     }
@@ -1071,7 +1090,7 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->node_of, h->Ah_csr, h->Ah_csc, h->Dr, h->Dc, h->normA, h->lbh, h->ubh,
                     h->rlh, h->ruh, h->ch, h->qh, h->x, h->x0, h->xe, h->xt, h->aty, h->aty0,
                     h->y, h->y0, h->yt, h->omega, h->part, h->part_node, h->pl_col_k,
-                    h->pl_col_r, h->pl_row_k, h->pl_row_c};
+                    h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;

@@ -8,18 +8,20 @@ from mpisppy_amd import _lib
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 cm = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 lanes = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
+extra = dict(kv.split('=') for kv in sys.argv[4].split(',')) if len(sys.argv) > 4 else {}
+extra = {k: (float(v) if '.' in v or 'e' in v else int(v)) for k, v in extra.items()}
 names = farmer.scenario_names_creator(S)
 b = farmer.batch_creator(names, crops_multiplier=cm, num_scens=S)
 ref = None
 for L in lanes:
-    for kern in ([1, 2] if L == lanes[0] else [2]):
+    for kern in ([1, 2] if (L == lanes[0] and not extra) else [2]):
         if L:
             os.environ["PHGPU_LANES"] = str(L)
         else:
             os.environ.pop("PHGPU_LANES", None)
         e = PHEngine(b, device="cuda:0")
         info = e.kernel_info()
-        o = _lib.default_options(kernel=kern)
+        o = _lib.default_options(kernel=kern, **extra)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record(); e.solve(o, warm=False); ev[1].record(); torch.cuda.synchronize()
         t0 = ev[0].elapsed_time(ev[1]); it0 = e.host("iters")
