@@ -120,9 +120,17 @@ def main():
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # RCCL ("nccl") by default; PHGPU_DIST_BACKEND=gloo lets several ranks share one
+        # GPU (functional rehearsal of the multi-rank path on a 1-GPU box)
+        backend = os.environ.get("PHGPU_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    local_rank = local_rank % max(1, ndev)
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     from mpisppy_amd.comm import Comm
@@ -156,7 +164,8 @@ def main():
         ev[1].record()
         ph.solve_loop(solver_options=ph.current_solver_options)
         ev[2].record()
-        return ev, conv
+        # scenario-iterations this launch processed (device-side sum, read after the timed region)
+        return ev, conv, ph.engine.iters.sum(dtype=torch.int64)
 
     for _ in range(a.warmup):
         step()
@@ -169,9 +178,11 @@ def main():
     torch.cuda.synchronize()
     comm.Barrier()
     elapsed = time.perf_counter() - t0
-    for (ev, conv) in evs:
+    units_per_step = []
+    for (ev, conv, its) in evs:
         red_ms.append(ev[0].elapsed_time(ev[1]))
         solve_ms.append(ev[1].elapsed_time(ev[2]))
+        units_per_step.append(float(its.item()))
     it_host = e.iters.cpu().numpy()
     pdhg_iters = (int(it_host.max()), float(it_host.mean()))
     t = torch.tensor([elapsed], dtype=torch.float64, device=e.device)
@@ -189,14 +200,17 @@ def main():
     if world == 1 and os.path.exists(pmc):
         try:
             d = json.load(open(pmc))
-            if ("void " + kname) in d["kernels"]:
-                traffic = d["k_solve_reg_traffic_bytes_per_launch"]["total_upper"]
+            tr = d.get("solve_traffic_bytes_per_launch", {}).get("void " + kname)
+            if tr is not None:
+                traffic = tr["total_upper"]
                 traffic_src = os.path.relpath(pmc, ROOT)
         except Exception:
             traffic = None
     B = 8 * (nnz + 5 * n + 4 * m + 3 * nn)           # SURVEY.md 8(d), per PDHG iter per scenario
-    units = float(it_host.sum())                     # scenario-iterations of the last launch
-    solve_s = float(np.mean(solve_ms[-1:])) / 1e3
+    # average over the K timed launches (HIP events on the launch stream); the rocprofv3
+    # kernel trace of the same command gives the per-dispatch durations (profiles/)
+    units = float(np.mean(units_per_step))           # scenario-iterations per launch
+    solve_s = float(np.mean(solve_ms)) / 1e3
     achieved = B * units / solve_s / 1e9
     ph_its = a.steps / elapsed
     status_ok = bool((e.status.cpu().numpy() == 0).all())

@@ -542,6 +542,37 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
         lb[t] = b;
     }
     __syncthreads();
+    // fast path (every two-stage problem, and any nonant whose local scenarios share one
+    // node): all runs belong to thread 0's node -> fixed-order tree sum
+    __shared__ int single;
+    if (t == 0) single = 1;
+    __syncthreads();
+    {
+        const int g0 = fnode[0] >= 0 ? fnode[0] : lnode[0];
+        if ((fnode[t] >= 0 && fnode[t] != g0) || (lnode[t] >= 0 && lnode[t] != g0)) single = 0;
+    }
+    __syncthreads();
+    if (single) {
+        fa[t] += la[t];
+        fb[t] += lb[t];
+        __syncthreads();
+        for (int off = XF_THREADS / 2; off > 0; off >>= 1) {
+            if (t < off) {
+                fa[t] += fa[t + off];
+                fb[t] += fb[t + off];
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            int g0 = -1;
+            for (int u = 0; u < XF_THREADS && g0 < 0; ++u) g0 = fnode[u] >= 0 ? fnode[u] : lnode[u];
+            if (g0 >= 0) {
+                node_buf[g0 * st.nlen_max + off] += fa[0];
+                node_buf[half + g0 * st.nlen_max + off] += fb[0];
+            }
+        }
+        return;
+    }
     if (t == 0) {
         int c = -1;
         double sa = 0.0, sb = 0.0;
