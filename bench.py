@@ -119,8 +119,10 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
     ndev = torch.cuda.device_count()
+    # several ranks may share one GPU in the gloo rehearsal (PHGPU_DIST_BACKEND=gloo)
+    local_rank = local_rank % max(1, ndev)
+    torch.cuda.set_device(local_rank)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         # RCCL ("nccl") by default; PHGPU_DIST_BACKEND=gloo lets several ranks share one
@@ -130,7 +132,6 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
-    local_rank = local_rank % max(1, ndev)
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     from mpisppy_amd.comm import Comm

@@ -1050,20 +1050,20 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_k = h->pl_row_k;
         pl.row_c = h->pl_row_c;
         const int G = WAVE / pl.L;
-        const size_t lds = (size_t)G * (size_t)(h->n + h->m + 2) * sizeof(double);
+        const size_t lds = (size_t)REG_WPB * G * (size_t)(h->n + h->m + 2) * sizeof(double);
         const reg_kernel_t fn = g_reg_instances[h->reg_inst].fn;
-        // persistent grid: co-resident single-wave workgroups (occupancy x CUs), never
-        // more than there are scenario groups
+        // persistent grid: co-resident workgroups of REG_WPB independent waves (occupancy
+        // x CUs), never more than there are scenario groups
         int per_cu = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, WAVE, lds));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, WAVE * REG_WPB, lds));
         if (per_cu < 1) per_cu = 1;
-        const int64_t need = (h->S + G - 1) / G;
+        const int64_t need = (h->S + (int64_t)G * REG_WPB - 1) / ((int64_t)G * REG_WPB);
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > need) nblk = need;
-        const int64_t first_dyn = nblk * G;
+        const int64_t first_dyn = nblk * REG_WPB * G;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
-        hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE), lds, st, *h, P, pl, h->qhead, first_dyn, x, y,
-                           obj, bound, status, iters);
+        hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE * REG_WPB), lds, st, *h, P, pl, h->qhead, first_dyn,
+                           x, y, obj, bound, status, iters);
     } else {
         hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
     }

@@ -1,0 +1,71 @@
+"""Summarise rocprofv3 --pmc SQ passes of the solve kernel (issue-side roofline).
+
+usage: python tools/pmc_sq_summary.py out.json passA.csv [passB.csv ...]
+
+For every counter the mean over the solve dispatches after the first (the first is the
+cold Iter0 LP) is reported, then derived figures:
+  valu_insts_per_wave          SQ_INSTS_VALU / SQ_WAVES
+  valu_busy                    4*SQ_ACTIVE_INST_VALU / (SIMDs * cycles): share of SIMD
+                               issue cycles spent on VALU (SQ_ACTIVE_INST_* count
+                               quad-cycles; cycles = GRBM_GUI_ACTIVE / 8 XCDs,
+                               MI355X_MICROARCH.md "DVFS give-back")
+  fp64_flops                   64 lanes * (2*FMA + ADD + MUL + TRANS) F64 instructions
+                               (upper bound: inactive lanes are counted)
+  fp64_tflops / fp64_frac      against the 78.6 TF fp64 vector peak (MI355X spec)
+"""
+import collections
+import csv
+import json
+import sys
+
+SIMDS = 256 * 4
+FP64_PEAK_TF = 78.6
+
+out_json, paths = sys.argv[1], sys.argv[2:]
+vals = collections.defaultdict(list)
+durs = []
+name = None
+for p in paths:
+    rows = [r for r in csv.DictReader(open(p)) if "k_solve" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    per = collections.defaultdict(dict)
+    for r in rows:
+        per[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+        per[int(r["Dispatch_Id"])]["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        name = r["Kernel_Name"].split("(")[0]
+    ids = sorted(per)[1:] or sorted(per)
+    for i in ids:
+        for k, v in per[i].items():
+            vals[k].append(v)
+mean = {k: sum(v) / len(v) for k, v in vals.items()}
+res = {"kernel": name, "counters_mean_per_dispatch": mean}
+d = {}
+if "SQ_INSTS_VALU" in mean and "SQ_WAVES" in mean:
+    d["valu_insts_per_wave"] = mean["SQ_INSTS_VALU"] / mean["SQ_WAVES"]
+if "SQ_INSTS_LDS" in mean and "SQ_WAVES" in mean:
+    d["lds_insts_per_wave"] = mean["SQ_INSTS_LDS"] / mean["SQ_WAVES"]
+if "GRBM_GUI_ACTIVE" in mean:
+    cyc = mean["GRBM_GUI_ACTIVE"] / 8.0
+    d["cycles"] = cyc
+    d["clock_GHz"] = cyc / mean["_dur_ns"]
+    if "SQ_ACTIVE_INST_VALU" in mean:
+        d["valu_busy"] = 4.0 * mean["SQ_ACTIVE_INST_VALU"] / (SIMDS * cyc)
+    if "SQ_ACTIVE_INST_LDS" in mean:
+        d["lds_issue_busy"] = 4.0 * mean["SQ_ACTIVE_INST_LDS"] / (SIMDS * cyc)
+    if "SQ_WAVE_CYCLES" in mean:
+        d["mean_waves_per_simd"] = 4.0 * mean["SQ_WAVE_CYCLES"] / (SIMDS * cyc)
+    if "SQ_WAIT_INST_LDS" in mean and "SQ_WAVE_CYCLES" in mean:
+        d["wave_frac_waiting_lds"] = mean["SQ_WAIT_INST_LDS"] / mean["SQ_WAVE_CYCLES"]
+    if "SQ_WAIT_ANY" in mean and "SQ_WAVE_CYCLES" in mean:
+        d["wave_frac_waiting_any"] = mean["SQ_WAIT_ANY"] / mean["SQ_WAVE_CYCLES"]
+f64 = [mean.get(k) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                             "SQ_INSTS_VALU_TRANS_F64")]
+if all(v is not None for v in f64):
+    fl = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
+    d["fp64_flops_per_dispatch"] = fl
+    d["fp64_tflops"] = fl / mean["_dur_ns"] / 1e3
+    d["fp64_frac_of_peak"] = d["fp64_tflops"] / FP64_PEAK_TF
+res["derived"] = d
+res["dispatch_ms_mean"] = mean.get("_dur_ns", 0) / 1e6
+json.dump(res, open(out_json, "w"), indent=1)
+print(json.dumps(res, indent=1))
