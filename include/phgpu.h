@@ -145,13 +145,22 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
                     double* W, const double* rho, int update_W, double* conv_local,
                     void* stream);
 
-/* Local probability-weighted sums (spopt.py:310-439) into out[4]:
+/* Local probability-weighted sums (spopt.py:310-439) into out[5]:
  *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
  *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s feasible} prob_s, where feasible
  *   means status is OPTIMAL or ITER_LIMIT (a solution was loaded; spopt.py:175-194
- *   marks only infeasible / unbounded / no-solution results infeasible) */
+ *   marks only infeasible / unbounded / no-solution results infeasible)
+ *   out[4] = sum_{s OPTIMAL} prob_s (certified solves: the xhat inner bound,
+ *   xhatbase.py:210-216, is only taken when this equals E1) */
 int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
                        const int32_t* status, double* out, void* stream);
+
+/* Fix the nonants of every local scenario (lb = ub = xfix[k*S + s], original units,
+ * clipped to the model bounds) for the following solves, or restore the model bounds
+ * when xfix is NULL.  Replaces SPOpt._fix_nonants / _restore_nonants as used by
+ * Xhat_Eval and XhatBase._try_one (spopt.py:557-660, xhatbase.py:199-216).
+ *   xfix: device [nn*S] (read during the call only) or NULL */
+int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* stream);
 
 /* Free the workspace and the handle. */
 int phgpu_destroy(phgpu_handle h);

@@ -65,7 +65,7 @@ struct phgpu_state {
     double *x, *x0, *xe, *xt, *aty, *aty0, *y, *y0, *yt;
     double* omega;
     // reductions
-    double* part;       // [nwaves * max(2*nn, 4)]
+    double* part;       // [nwaves * max(2*nn, 5)]
     int32_t* part_node; // [nwaves * nn]
     int64_t nwaves;
     int64_t ws_bytes;
@@ -623,24 +623,46 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
     if ((threadIdx.x & (WAVE - 1)) == 0) st.part[s / WAVE] = acc;
 }
 
-// spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible.
+// spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible, prob*optimal.
 __global__ void __launch_bounds__(BLOCK)
 k_expect_partial(phgpu_state st, const double* __restrict__ obj, const double* __restrict__ bound,
                  const int32_t* __restrict__ status) {
     const int64_t S = st.S;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     if (s < S) {
         const double p = st.prob[s];
         v[0] = p * obj[s];
         v[1] = p * bound[s];
         v[2] = p;
         v[3] = (status[s] == PHGPU_OPTIMAL || status[s] == PHGPU_ITER_LIMIT) ? p : 0.0;
+        v[4] = (status[s] == PHGPU_OPTIMAL) ? p : 0.0;
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 5; ++t) {
         const double a = wave_sum(v[t]);
-        if ((threadIdx.x & (WAVE - 1)) == 0) st.part[(s / WAVE) * 4 + t] = a;
+        if ((threadIdx.x & (WAVE - 1)) == 0) st.part[(s / WAVE) * 5 + t] = a;
+    }
+}
+
+// Xhat_Eval._fix_nonants (utils/xhat_eval.py; spopt.py _fix_nonants): nonant columns of
+// every scenario get lb = ub = xfix[k, s] (scaled); xfix == NULL restores the model bounds.
+__global__ void __launch_bounds__(BLOCK)
+k_fix_nonants(phgpu_state st, const double* __restrict__ xfix) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    for (int k = 0; k < st.nn; ++k) {
+        const int j = st.nonant_col[k];
+        const double d = st.Dc[IX(j)];
+        if (xfix) {
+            const double v = fmin(fmax(xfix[IX(k)], st.lb[IX(j)]), st.ub[IX(j)]);
+            st.lbh[IX(j)] = v / d;
+            st.ubh[IX(j)] = v / d;
+        } else {
+            st.lbh[IX(j)] = st.lb[IX(j)] / d;
+            st.ubh[IX(j)] = st.ub[IX(j)] / d;
+        }
     }
 }
 
@@ -879,7 +901,7 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
         h->num_cus = ncu;
     }
     {
-        size_t K = (size_t)(2 * nn > 4 ? 2 * nn : 4);
+        size_t K = (size_t)(2 * nn > 5 ? 2 * nn : 5);
         ALLOC(h->part, (size_t)h->nwaves * K);
         ALLOC(h->part_node, (size_t)h->nwaves * (nn > 0 ? nn : 1));
     }
@@ -1107,8 +1129,17 @@ extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const doubl
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_expect_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, obj, bound, status);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_sum_partials, dim3(4), dim3(256), 0, st, (const double*)h->part, h->nwaves, 4, 1.0,
+    hipLaunchKernelGGL(k_sum_partials, dim3(5), dim3(256), 0, st, (const double*)h->part, h->nwaves, 5, 1.0,
                        out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* stream) {
+    if (!h) return set_err(-1, "null handle");
+    if (h->nn == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_fix_nonants, grid_for(h->S), dim3(BLOCK), 0, st, *h, xfix);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -95,7 +95,8 @@ class PHEngine:
         self.xbar = z(max(nn, 1), S)
         self.node_buf = z(2 * self.num_nodes * self.nlen_max)
         self.conv_buf = z(1)
-        self.exp_buf = z(4)
+        self.exp_buf = z(5)
+        self.xfix = None
         self.W_on = 0
         self.prox_on = 0
         self._upload()
@@ -187,12 +188,40 @@ class PHEngine:
         return float(self.conv_buf.item()) / self.comm.size
 
     def expectations(self):
-        """(Eobj, Ebound, E1, Efeas) summed over ranks (spopt.py:310-439)."""
+        """(Eobj, Ebound, E1, Efeas, Eoptimal) summed over ranks (spopt.py:310-439)."""
         _lib.check(self.lib.phgpu_expectations(self.h, _ptr(self.obj), _ptr(self.bound), _ptr(self.status),
                                                _ptr(self.exp_buf), self._stream()), "phgpu_expectations")
         self.comm.allreduce_sum_(self.exp_buf)
         v = self.exp_buf.cpu().numpy()
-        return float(v[0]), float(v[1]), float(v[2]), float(v[3])
+        return float(v[0]), float(v[1]), float(v[2]), float(v[3]), float(v[4])
+
+    def fix_nonants(self, xfix):
+        """lb = ub = xfix on the nonant columns of every local scenario (device [nn, S]
+        tensor, original units) for the next solves; None restores the model bounds
+        (spopt.py:557-660 _fix_nonants / _restore_nonants)."""
+        if xfix is not None:
+            self.xfix = xfix.to(device=self.device, dtype=torch.float64).contiguous()
+            assert tuple(self.xfix.shape) == (max(self.nn, 1), self.S), self.xfix.shape
+        else:
+            self.xfix = None
+        _lib.check(self.lib.phgpu_fix_nonants(self.h, _ptr(self.xfix), self._stream()), "phgpu_fix_nonants")
+
+    def fix_nonants_by_node(self, table):
+        """Fix every local scenario's nonants at per-node values: ``table`` is a device
+        [num_nodes, nlen_max] tensor (global node order of ``node_names``); nonant k of
+        scenario s gets table[node_of[depth_k, s], off_k] (the per-node cache of
+        spopt.py:557-592)."""
+        if not hasattr(self, "_fix_index"):
+            d = torch.as_tensor(self.batch.nonant_depth, dtype=torch.long, device=self.device)
+            o = torch.as_tensor(self.batch.nonant_off, dtype=torch.long, device=self.device)
+            self._fix_index = self.node_of.long().index_select(0, d) * self.nlen_max + o[:, None]
+        t = table.reshape(-1).to(device=self.device, dtype=torch.float64)
+        self.fix_nonants(t[self._fix_index])
+
+    def nonant_x_dev(self):
+        """[nn, S] device tensor of the nonant values of the last solve."""
+        idx = torch.as_tensor(self.batch.nonant_col, dtype=torch.long, device=self.device)
+        return self.x.index_select(0, idx)
 
     # -------------------------------------------------------------- host views
     def nonant_x(self):

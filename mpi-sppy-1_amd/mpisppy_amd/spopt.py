@@ -45,9 +45,15 @@ class SPOpt(SPBase):
             self.engine = PHEngine(self.batch, device=self.options.get("device"), comm=self.mpicomm,
                                    node_names=self.node_names)
 
+    # options the reference's cfg_vanilla.shared_options passes to MIP/LP plugins
+    # (threads, mipgap; cfg_vanilla.py:41-62) or that only drive plugin output (Tee):
+    # meaningless for PDHG, accepted and ignored; any other unknown key raises
+    FOREIGN_SOLVER_OPTIONS = ("threads", "mipgap", "Tee", "tee", "timelimit", "time_limit")
+
     @staticmethod
     def _to_phgpu_options(solver_options):
-        return _lib.default_options(**(solver_options or {}))
+        so = {k: v for k, v in (solver_options or {}).items() if k not in SPOpt.FOREIGN_SOLVER_OPTIONS}
+        return _lib.default_options(**so)
 
     # spopt.py:226-307
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,

@@ -82,3 +82,66 @@ def option_string_to_dict(ostr):
         else:
             raise RuntimeError("Illegally formed subsolve directive option=%s detected" % this_option_string)
     return solver_options
+
+
+class TreeNode:
+    """Non-leaf / leaf node of the scenario tree with the contiguous range of scenario
+    indices below it (the scenfirst / scenlast / kids / is_leaf of sputils._TreeNode,
+    sputils.py:672-726)."""
+
+    def __init__(self, name, stage, scenfirst, scenlast):
+        self.name = name
+        self.stage = stage
+        self.scenfirst = scenfirst
+        self.scenlast = scenlast
+        self.kids = []
+
+    @property
+    def is_leaf(self):
+        return not self.kids
+
+
+def scenario_tree(all_nodenames, num_scens):
+    """{name: TreeNode} for every node of all_nodenames (sputils._ScenTree, 743-772).
+
+    Two-stage (all_nodenames None or ['ROOT']): ROOT spans all scenarios and has no kids.
+    Multistage: leaves are the nodes without a child '<name>_0'; every leaf is one
+    scenario and a node's scenarios are its descendant leaves, in name order."""
+    if all_nodenames is None or list(all_nodenames) == ["ROOT"]:
+        return {"ROOT": TreeNode("ROOT", 1, 0, num_scens - 1)}
+    names = set(all_nodenames)
+
+    def children(nd):
+        out = []
+        i = 0
+        while f"{nd}_{i}" in names:
+            out.append(f"{nd}_{i}")
+            i += 1
+        return out
+
+    nodes = {}
+
+    def build(nd, stage, first):
+        kids = children(nd)
+        if not kids:
+            nodes[nd] = TreeNode(nd, stage, first, first)
+            return first + 1
+        nxt = first
+        for k in kids:
+            nxt = build(k, stage + 1, nxt)
+        node = TreeNode(nd, stage, first, nxt - 1)
+        node.kids = [nodes[k] for k in kids]
+        nodes[nd] = node
+        return nxt
+
+    last = build("ROOT", 1, 0)
+    if last != num_scens:
+        raise RuntimeError(f"The all_nodenames argument gives {last} leaves for {num_scens} scenarios")
+    ordered = {}
+
+    def preorder(t):          # _ScenTree.nonleaves order: node, then its subtrees
+        ordered[t.name] = t
+        for k in t.kids:
+            preorder(k)
+    preorder(nodes["ROOT"])
+    return ordered
