@@ -926,15 +926,14 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
         phgpu_destroy(h);
         return set_err(-2, "pattern upload failed: %s", hipGetErrorString(e));
     }
-    // register-resident path: lanes per scenario L (power of two <= 64).  Smallest L
-    // with a fitting instance, doubled while the grid has fewer than 4 lanes per
-    // (SIMD lane x wave slot) of the chip and a scenario still has columns to spread.
+    // register-resident path: lanes per scenario L (power of two <= 64): the smallest L
+    // with a fitting instance, doubled while S * L lanes would not fill REG_WAVES_PER_EU
+    // waves on every SIMD of the chip and a scenario still has columns to spread
+    // (measured on farmer cm=1: L=4 at S >= 32768, 8 at 16384, 16 at 8192 -- profiles/r01);
+    // PHGPU_LANES=<L> pins it (tuning / tests)
     h->reg_inst = -1;
     {
-        // lanes per scenario: the smallest L with a fitting instance, doubled while the
-        // grid holds fewer than 8 waves per SIMD of the chip and a scenario still has
-        // columns to spread; PHGPU_LANES=<L> pins it (tuning / tests)
-        const int64_t target = (int64_t)256 * 4 * WAVE * 8;
+        const int64_t target = (int64_t)h->num_cus * 4 * WAVE * REG_WAVES_PER_EU;
         const char* env = getenv("PHGPU_LANES");
         const int pinned = env ? atoi(env) : 0;
         int chosen = -1;
@@ -1072,7 +1071,8 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_k = h->pl_row_k;
         pl.row_c = h->pl_row_c;
         const int G = WAVE / pl.L;
-        const size_t lds = (size_t)REG_WPB * G * (size_t)(h->n + h->m + 2) * sizeof(double);
+        const reg_instance& ri = g_reg_instances[h->reg_inst];
+        const size_t lds = (size_t)REG_WPB * reg_wave_lds(h->n, h->m, G, ri.KC, ri.KR) * sizeof(double);
         const reg_kernel_t fn = g_reg_instances[h->reg_inst].fn;
         // persistent grid: co-resident workgroups of REG_WPB independent waves (occupancy
         // x CUs), never more than there are scenario groups
