@@ -1,10 +1,12 @@
-# GPU validation: parity tests, then the bench + profiles, then a 2-rank rehearsal of the
-# multi-rank path on the one GPU (gloo between the ranks, both ranks on cuda:0)
+# GPU validation: parity tests, bench, kernel-trace stats, PMC passes (HBM bytes, SQ issue)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1
-rc=$?; echo "tests rc=$rc" >> gpurun_out/gputests.log; [ $rc -eq 0 ] || exit $rc
-bash gpu_bench.sh || exit $?
-PHGPU_DIST_BACKEND=gloo timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/bench2.log 2>&1
-echo "bench2 rc=$?" >> gpurun_out/bench2.log
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/gputests.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || exit $?
+python tools/trace_summary.py gpurun_out/prof/run_kernel_trace.csv 20 gpurun_out/prof/solve_dispatches.json >> gpurun_out/prof.log 2>&1
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_WAVES SQ_WAVE_CYCLES --output-format csv -d gpurun_out/pmc_sqa -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sqa.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_ANY --output-format csv -d gpurun_out/pmc_sqb -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sqb.log 2>&1 || exit $?

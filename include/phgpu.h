@@ -157,8 +157,10 @@ int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
 
 /* Fix the nonants of every local scenario (lb = ub = xfix[k*S + s], original units,
  * clipped to the model bounds) for the following solves, or restore the model bounds
- * when xfix is NULL.  Replaces SPOpt._fix_nonants / _restore_nonants as used by
- * Xhat_Eval and XhatBase._try_one (spopt.py:557-660, xhatbase.py:199-216).
+ * when xfix is NULL.  A NaN entry leaves that nonant at its model bounds (partial
+ * fixing: Xhat_Eval.fix_nonants_upto_stage, xhat_eval.py:326-362).  Replaces
+ * SPOpt._fix_nonants / _restore_nonants as used by Xhat_Eval and XhatBase._try_one
+ * (spopt.py:557-660, xhatbase.py:199-216).
  *   xfix: device [nn*S] (read during the call only) or NULL */
 int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* stream);
 

@@ -655,8 +655,9 @@ k_fix_nonants(phgpu_state st, const double* __restrict__ xfix) {
     for (int k = 0; k < st.nn; ++k) {
         const int j = st.nonant_col[k];
         const double d = st.Dc[IX(j)];
-        if (xfix) {
-            const double v = fmin(fmax(xfix[IX(k)], st.lb[IX(j)]), st.ub[IX(j)]);
+        const double xv = xfix ? xfix[IX(k)] : NAN;
+        if (!isnan(xv)) {
+            const double v = fmin(fmax(xv, st.lb[IX(j)]), st.ub[IX(j)]);
             st.lbh[IX(j)] = v / d;
             st.ubh[IX(j)] = v / d;
         } else {

@@ -50,6 +50,13 @@ class Comm:
         dist.broadcast_object_list(lst, src=root, group=self.group)
         return lst[0]
 
+    def allgather_object(self, obj):
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
     def gather_object(self, obj, root=0):
         if self.size == 1:
             return [obj]

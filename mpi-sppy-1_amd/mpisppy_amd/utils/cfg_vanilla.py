@@ -1,5 +1,6 @@
 """Cylinder dict builders (mirrors mpisppy/utils/cfg_vanilla.py:41-495 for the cylinders
-this engine serves: ph_hub, lagrangian_spoke, xhatshuffle_spoke).
+this engine serves: ph_hub, lagrangian_spoke, xhatshuffle_spoke; extension_adder and
+add_wxbar_read_write for the hub's extensions).
 
 ``cfg`` is any object with the reference's config attribute names (solver_name,
 default_rho, max_iterations, rel_gap, ...); missing attributes take the reference's
@@ -10,9 +11,12 @@ import copy
 from ..cylinders.hub import PHHub
 from ..cylinders.lagrangian_bounder import LagrangianOuterBound
 from ..cylinders.xhatshufflelooper_bounder import XhatShuffleInnerBound
+from ..extensions.extension import MultiExtension
 from ..opt.ph import PH
 from ..phbase import PHBase
 from .xhat_eval import Xhat_Eval
+from .wxbarreader import WXBarReader
+from .wxbarwriter import WXBarWriter
 
 
 def _get(cfg, name, default=None):
@@ -117,3 +121,38 @@ def xhatshuffle_spoke(cfg, scenario_creator, scenario_denouement, all_scenario_n
             "all_nodenames": all_nodenames,
         },
     }
+
+
+# cfg_vanilla.py:164-181
+def extension_adder(hub_dict, ext_class):
+    ok = hub_dict["opt_kwargs"]
+    if ok.get("extensions") is None:
+        ok["extensions"] = ext_class
+    elif ok["extensions"] == MultiExtension:
+        if ok.get("extension_kwargs") is None:
+            ok["extension_kwargs"] = {"ext_classes": []}
+        if ext_class not in ok["extension_kwargs"]["ext_classes"]:
+            ok["extension_kwargs"]["ext_classes"].append(ext_class)
+    elif ok["extensions"] != ext_class:
+        ok["extension_kwargs"] = {"ext_classes": [ok["extensions"], ext_class]}
+        ok["extensions"] = MultiExtension
+    return hub_dict
+
+
+# cfg_vanilla.py:202-224 (options stay loose in the hub's options dict, as there)
+def add_wxbar_read_write(hub_dict, cfg):
+    if getattr(cfg, "init_W_fname", None) is not None or getattr(cfg, "init_Xbar_fname", None) is not None:
+        hub_dict = extension_adder(hub_dict, WXBarReader)
+        hub_dict["opt_kwargs"]["options"].update({
+            "init_W_fname": getattr(cfg, "init_W_fname", None),
+            "init_Xbar_fname": getattr(cfg, "init_Xbar_fname", None),
+            "init_separate_W_files": bool(getattr(cfg, "init_separate_W_files", False)),
+        })
+    if getattr(cfg, "W_fname", None) is not None or getattr(cfg, "Xbar_fname", None) is not None:
+        hub_dict = extension_adder(hub_dict, WXBarWriter)
+        hub_dict["opt_kwargs"]["options"].update({
+            "W_fname": getattr(cfg, "W_fname", None),
+            "Xbar_fname": getattr(cfg, "Xbar_fname", None),
+            "separate_W_files": bool(getattr(cfg, "separate_W_files", False)),
+        })
+    return hub_dict

@@ -92,12 +92,74 @@ class Xhat_Eval(SPOpt):
             return None
         return self.Eobjective(self.verbose, fct=fct)
 
+    # xhat_eval.py:261-291
+    def evaluate_one(self, nonant_cache, scenario_name, s=None):
+        """Objective of one scenario with its nonants fixed at ``nonant_cache`` (None if
+        that solve is not certified optimal).  The batched engine solves every local
+        scenario in the one launch; the others' results are simply not read."""
+        self._lazy_create_solvers()
+        self._fix_nonants(nonant_cache)
+        self.solve_loop(solver_options=self.options.get("solver_options"), gripe=True)
+        k = self.local_scenario_names.index(scenario_name)
+        if int(self.engine.status[k].item()) != 0:
+            return None
+        obj = float(self.engine.obj[k].item())
+        if not hasattr(self, "objs_dict"):
+            self.objs_dict = {}
+        self.objs_dict[scenario_name] = obj
+        return obj
+
+    # xhat_eval.py:326-362
+    def fix_nonants_upto_stage(self, t, cache):
+        """Fix the nonants of the nodes of stages 1..t at ``cache`` ({node: values});
+        later stages keep their model bounds (NaN entries of the device fix table)."""
+        self._lazy_create_solvers()
+        e = self.engine
+        depth = np.asarray(self.batch.nonant_depth)
+        need = {nd for nd, st in zip(e.node_names, self._node_stages()) if st <= t}
+        for nd in need:
+            if nd not in cache:
+                raise RuntimeError(f"Could not find {nd} in {cache}")
+            if cache[nd] is None:
+                raise RuntimeError(f"Empty cache for node={nd}")
+            want = self._node_len(nd)
+            if len(cache[nd]) != want:
+                raise RuntimeError(f"Needed {want} nonant Vars for {nd}, got {len(cache[nd])}")
+        tab = self._node_table({nd: cache[nd] for nd in need})
+        if not hasattr(e, "_fix_index"):
+            e.fix_nonants_by_node(tab)          # builds the index once
+        xfix = tab.reshape(-1)[e._fix_index].clone()
+        late = torch.as_tensor(depth + 1 > t, device=e.device)
+        xfix[late] = float("nan")
+        e.fix_nonants(xfix)
+        self._fixed = True
+
+    def _node_stages(self):
+        """Stage (1 + tree depth) of each engine node held by a local scenario; nodes
+        no local scenario passes through get a stage past the tree (never fixed here)."""
+        node_of = self.engine.node_of.cpu().numpy()          # [depth, S] global node ids
+        stages = [10 ** 9] * self.engine.num_nodes
+        for d in range(node_of.shape[0]):
+            for g in np.unique(node_of[d]):
+                stages[int(g)] = d + 1
+        return stages
+
+    def _node_len(self, nd):
+        d = self._node_stages()[self.engine.node_names.index(nd)] - 1
+        return int(np.sum(np.asarray(self.batch.nonant_depth) == d))
+
+    # xhat_eval.py:368-400
+    def _fix_nonants_at_value(self):
+        """Fix every nonant at its current (last-solve) value."""
+        self._lazy_create_solvers()
+        self.engine.fix_nonants(self.engine.nonant_x_dev())
+        self._fixed = True
+
     # xhat_eval.py:402-434 (fix at the current values, solve, E[obj] or None)
     def calculate_incumbent(self, fix_nonants=True, verbose=False):
         self._lazy_create_solvers()
         if fix_nonants:
-            self.engine.fix_nonants(self.engine.nonant_x_dev())
-            self._fixed = True
+            self._fix_nonants_at_value()
         self.solve_loop(solver_options=self.options.get("iterk_solver_options"), verbose=verbose)
         if self.infeas_prob() > 1e-12:
             return None

@@ -49,6 +49,8 @@ def xhat_objective(scens, node_values):
         A, rl, ru, lb, ub, c, q = s.arrays()
         xf = np.full(len(c), np.nan)
         for (ndn, _cond, _stage, idx) in s.nodes:
+            if ndn not in node_values:          # partial fix (fix_nonants_upto_stage)
+                continue
             v = np.asarray(node_values[ndn], dtype=float)
             for o, j in enumerate(idx):
                 xf[j] = min(max(v[o], lb[j]), ub[j])
