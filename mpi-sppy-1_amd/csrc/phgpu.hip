@@ -691,6 +691,22 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__
 // columns j = l + q L and rows i = l + r L; each column's CSC entries and each row's
 // CSR entries are padded to the instance's ZC / ZR slots.  Returns false if no
 // compiled instance fits (then the global-memory kernel is used).
+// register-cost estimate of an instance, in doubles per lane
+static inline long reg_cost(const reg_instance& r) {
+    return (long)r.KC * (13 + r.ZC) + (long)r.KR * (7 + r.ZR);
+}
+
+// an instance that spills more than REG_SPILL_MAX bytes of scratch per lane at 2 waves /
+// SIMD is skipped by the lane search (L doubles past it).  Measured on farmer 65,536 cm=1
+// (profiles/r01): <8,4,4,4> at L=2 spills 1.5 KB -> 14.4 ms per solve; <3,3,2,4> at L=4
+// spills 68 B -> 0.67 ms; <2,3,1,4> at L=8, no spill -> 0.77 ms.
+#define REG_SPILL_MAX 128
+static bool reg_spills(const reg_instance& r) {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, (const void*)r.fn) != hipSuccess) return false;
+    return a.localSizeBytes > REG_SPILL_MAX;
+}
+
 static bool build_plan(int L, int n, int m, const int32_t* row_ptr, const int32_t* col_idx,
                        int* inst_out, int* kc_out, int* zc_out, int* kr_out, int* zr_out,
                        std::vector<int32_t>& col_k, std::vector<int32_t>& col_r,
@@ -710,8 +726,7 @@ static bool build_plan(int L, int n, int m, const int32_t* row_ptr, const int32_
     for (int a = 0; a < ninst; ++a) {
         const reg_instance& r = g_reg_instances[a];
         if (r.KC >= kc && r.ZC >= zc && r.KR >= kr && r.ZR >= zr) {
-            // register-cost estimate in doubles per lane
-            const long cost = (long)r.KC * (13 + r.ZC) + (long)r.KR * (7 + r.ZR);
+            const long cost = reg_cost(r);
             if (inst < 0 || cost < best) {
                 inst = a;
                 best = cost;
@@ -930,7 +945,8 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
     // register-resident path: lanes per scenario L (power of two <= 64): the smallest L
     // with a fitting instance, doubled while S * L lanes would not fill REG_WAVES_PER_EU
     // waves on every SIMD of the chip and a scenario still has columns to spread
-    // (measured on farmer cm=1: L=4 at S >= 32768, 8 at 16384, 16 at 8192 -- profiles/r01);
+    // (measured on farmer cm=1: L=4 at S >= 32768, 8 at 16384, 16 at 8192 -- profiles/r01),
+    // and past any L whose instance spills (reg_spills);
     // PHGPU_LANES=<L> pins it (tuning / tests)
     h->reg_inst = -1;
     {
@@ -938,6 +954,7 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
         const char* env = getenv("PHGPU_LANES");
         const int pinned = env ? atoi(env) : 0;
         int chosen = -1;
+        bool chosen_spills = false;
         std::vector<int32_t> ck, cr, rk, rc;
         int inst = -1, kc = 0, zc = 0, kr = 0, zr = 0;
         for (int L = 1; L <= WAVE; L *= 2) {
@@ -945,8 +962,11 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
             std::vector<int32_t> a1, a2, a3, a4;
             int i1, i2, i3, i4, i5;
             if (!build_plan(L, n, m, row_ptr, col_idx, &i1, &i2, &i3, &i4, &i5, a1, a2, a3, a4)) continue;
-            if (pinned <= 0 && chosen >= 0 && (S * (int64_t)chosen >= target || chosen >= n)) break;
+            if (pinned <= 0 && chosen >= 0 && (S * (int64_t)chosen >= target || chosen >= n) &&
+                !chosen_spills)
+                break;
             chosen = L;
+            chosen_spills = reg_spills(g_reg_instances[i1]);
             inst = i1; kc = i2; zc = i3; kr = i4; zr = i5;
             ck.swap(a1); cr.swap(a2); rk.swap(a3); rc.swap(a4);
         }
