@@ -156,7 +156,11 @@ def main():
     pdhg_iters = []
     red_ms = []
 
-    def step():
+    # per-launch scenario-iterations for the roofline: a D2D snapshot of the iteration
+    # counts per step (one copy, no reduction kernel inside the timed region)
+    it_snap = torch.empty((a.warmup + a.steps, b.S), dtype=e.iters.dtype, device=e.device)
+
+    def step(k):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ev[0].record()
         ph.Compute_Xbar()
@@ -165,25 +169,24 @@ def main():
         ev[1].record()
         ph.solve_loop(solver_options=ph.current_solver_options)
         ev[2].record()
-        # scenario-iterations this launch processed (device-side sum, read after the timed region)
-        return ev, conv, ph.engine.iters.sum(dtype=torch.int64)
+        it_snap[k].copy_(ph.engine.iters)
+        return ev, conv
 
-    for _ in range(a.warmup):
-        step()
+    for k in range(a.warmup):
+        step(k)
     torch.cuda.synchronize()
     comm.Barrier()
     t0 = time.perf_counter()
     evs = []
-    for _ in range(a.steps):
-        evs.append(step())
+    for k in range(a.steps):
+        evs.append(step(a.warmup + k))
     torch.cuda.synchronize()
     comm.Barrier()
     elapsed = time.perf_counter() - t0
-    units_per_step = []
-    for (ev, conv, its) in evs:
+    units_per_step = it_snap[a.warmup:].sum(dim=1, dtype=torch.int64).cpu().tolist()
+    for (ev, conv) in evs:
         red_ms.append(ev[0].elapsed_time(ev[1]))
         solve_ms.append(ev[1].elapsed_time(ev[2]))
-        units_per_step.append(float(its.item()))
     it_host = e.iters.cpu().numpy()
     pdhg_iters = (int(it_host.max()), float(it_host.mean()))
     t = torch.tensor([elapsed], dtype=torch.float64, device=e.device)
@@ -207,6 +210,21 @@ def main():
                 traffic_src = os.path.relpath(pmc, ROOT)
         except Exception:
             traffic = None
+    # issue-side counters of the same kernel (rocprofv3 SQ_* passes, profiles/r01): what
+    # actually bounds it, since the iterate never streams through HBM
+    issue = None
+    sq = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_summary_farmer{a.scens}_cm{a.cm}.json")
+    if world == 1 and os.path.exists(sq):
+        try:
+            d = json.load(open(sq))
+            if d.get("kernel") == "void " + kname:
+                dv = d["derived"]
+                issue = {"valu_busy": dv["valu_busy"], "lds_issue_busy": dv["lds_issue_busy"],
+                         "mean_waves_per_simd": dv["mean_waves_per_simd"],
+                         "fp64_tflops": dv["fp64_tflops"], "fp64_frac_of_vector_peak": dv["fp64_frac_of_peak"],
+                         "source": os.path.relpath(sq, ROOT)}
+        except Exception:
+            issue = None
     B = 8 * (nnz + 5 * n + 4 * m + 3 * nn)           # SURVEY.md 8(d), per PDHG iter per scenario
     # average over the K timed launches (HIP events on the launch stream); the rocprofv3
     # kernel trace of the same command gives the per-dispatch durations (profiles/)
@@ -240,7 +258,7 @@ def main():
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "issue": issue,
                          "kernel": kname, "lanes_per_scenario": kinfo["lanes"],
                          "bytes_per_scenario_iter": B,
                          "scenario_iters_per_launch": units, "launch_ms": solve_s * 1e3,

@@ -4,6 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/gputests.log 2>&1 || exit $?
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 200 python -u tools/kbench.py 65536 1 0 > gpurun_out/kb_s65536.log 2>&1 || exit $?
 timeout -k 10 200 python -u tools/kbench.py 8192 1 0 > gpurun_out/kb_s8192.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
