@@ -62,7 +62,8 @@ typedef struct {
     double eps_abs;        /* absolute KKT tolerance                          [1e-12] */
     int32_t max_iter;      /* PDHG iteration cap per scenario                 [100000] */
     int32_t check_every;   /* KKT / restart check period (iterations)         [64] */
-    double gamma;          /* Halpern reflection coefficient in [0, 1]         [1.0] */
+    double gamma;          /* Halpern reflection coefficient in [0, 1]         [1.0]
+                              (kernel 2 requires 1.0; kernel 0 uses kernel 1 otherwise) */
     double beta_sufficient;/* restart if r <= beta_suff * r_restart           [0.2] */
     double beta_necessary; /* ... or r <= beta_nec * r_restart and no progress [0.8] */
     double eta_frac;       /* step = eta_frac / ||A_scaled||_2                [0.998] */

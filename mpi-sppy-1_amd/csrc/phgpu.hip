@@ -1077,9 +1077,13 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
     P.wmin = 1.0 / P.wmax;
     hipStream_t st = (hipStream_t)stream;
-    const bool use_reg = (o.kernel == 2) || (o.kernel == 0 && h->reg_inst >= 0);
+    // the register-resident kernel is specialised for the reflected step (gamma = 1, the
+    // default); another gamma runs on the global-memory kernel
+    const bool use_reg = (o.kernel == 2) || (o.kernel == 0 && h->reg_inst >= 0 && o.gamma == 1.0);
     if (o.kernel == 2 && h->reg_inst < 0)
         return set_err(-1, "register-resident kernel requested but no compiled instance fits this pattern");
+    if (o.kernel == 2 && o.gamma != 1.0)
+        return set_err(-1, "register-resident kernel requires gamma = 1 (got %g)", o.gamma);
     if (use_reg) {
         reg_plan pl;
         pl.L = h->reg_L;

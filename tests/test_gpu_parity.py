@@ -268,3 +268,23 @@ def test_register_kernel_on_random_batches(gpu):
         assert np.all(np.abs(o1 - o2) <= tol), (o1, o2)
         assert np.all(np.abs(e.host("bound") - b1) <= tol)
         e.close()
+
+
+def test_gamma_not_one_uses_global_kernel(gpu):
+    """The register-resident kernel is specialised for the reflected step (gamma = 1):
+    auto selection runs another gamma on the global-memory kernel, and forcing the
+    register kernel with it is a loud error."""
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    b = _random_lp_batch(37, 11, 7, 0.35, seed=5, with_q=False)
+    e = PHEngine(b, device="cuda:0")
+    assert e.kernel_info()["instance"] >= 0
+    e.solve(_lib.default_options(kernel=2), warm=False)
+    o_ref = e.host("obj").copy()
+    e.solve(_lib.default_options(kernel=0, gamma=0.5), warm=False)
+    assert (e.host("status") == 0).all()
+    tol = OBJ_REL * np.maximum(1.0, np.abs(o_ref))
+    assert np.all(np.abs(e.host("obj") - o_ref) <= tol)
+    with pytest.raises(_lib.PhgpuError):
+        e.solve(_lib.default_options(kernel=2, gamma=0.5), warm=False)
+    e.close()
