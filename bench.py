@@ -6,6 +6,7 @@ all-reduce) -> solve_loop (one batched PDHG solve over the rank's scenarios).
 Model generation, Iter0 and the warmup iterations are outside the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm CM]
+    python bench.py --model aircond --bf 32,32,64     # config 4 (multistage), not the headline
 
 N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL); scenarios are
 sharded contiguously (sputils.py:798-810); total scenarios are fixed (strong scaling).
@@ -17,11 +18,16 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-sppy-1_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "PH iterations/sec + scenario subproblem solves/sec, farmer 64K scen, 1–8 GPUs"
+# config 4 parameters (straight_tests.py:36)
+AIRCOND_KW = {"Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50, "mu_dev": 0, "sigma_dev": 40,
+              "start_seed": 0}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -32,6 +38,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--scens", type=int, default=65536)
     p.add_argument("--cm", type=int, default=1)
+    p.add_argument("--model", choices=["farmer", "aircond"], default="farmer",
+                   help="farmer (config 3, the headline) or aircond (config 4, multistage)")
+    p.add_argument("--bf", type=str, default="32,32,64",
+                   help="aircond branching factors (scenarios = their product)")
     p.add_argument("--rho", type=float, default=1.0)
     p.add_argument("--eps", type=float, default=1e-9)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,11 +122,13 @@ def main():
             raise SystemExit("for --gpus N > 1 launch with: python -m torch.distributed.run "
                              "--nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N")
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if a.model == "aircond":
+        a.bf = [int(v) for v in a.bf.split(",")]
+        a.scens = int(np.prod(a.bf))
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.model == "farmer":
         sample = a.cpu_sample or min(a.scens, 1024)
         cpu = cpu_baseline(a.scens, a.cm, a.rho, sample)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
@@ -137,14 +149,31 @@ def main():
     from mpisppy_amd.comm import Comm
 
     comm = Comm()
-    names = farmer.scenario_names_creator(a.scens)
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 1, "defaultPHrho": a.rho, "convthresh": -1.0,
             "verbose": False, "display_progress": False, "toc": False,
-            "device": f"cuda:{local_rank}", "batch_creator": farmer.batch_creator,
+            "device": f"cuda:{local_rank}",
             "iter0_solver_options": {"eps_rel": a.eps}, "iterk_solver_options": {"eps_rel": a.eps}}
     t_setup = time.perf_counter()
-    ph = PH(opts, names, farmer.scenario_creator, mpicomm=comm,
-            scenario_creator_kwargs={"crops_multiplier": a.cm, "num_scens": a.scens})
+    if a.model == "farmer":
+        names = farmer.scenario_names_creator(a.scens)
+        opts["batch_creator"] = farmer.batch_creator
+        ph = PH(opts, names, farmer.scenario_creator, mpicomm=comm,
+                scenario_creator_kwargs={"crops_multiplier": a.cm, "num_scens": a.scens})
+        tag = f"farmer{a.scens}_cm{a.cm}"
+        workload = {(65536, 1): "farmer PH (config 3)",
+                    (1024, 10): "farmer PH (config 2)"}.get((a.scens, a.cm), f"farmer PH, cm={a.cm}")
+    else:
+        # config 4: aircond multistage (aircond.py:37-330), default parameters, one
+        # scenario per leaf of the bf tree; per-node x̄ over all non-leaf nodes
+        from mpisppy_amd.examples import aircond
+        from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+        names = aircond.scenario_names_creator(a.scens)
+        opts["batch_creator"] = aircond.batch_creator
+        ph = PH(opts, names, aircond.scenario_creator, mpicomm=comm,
+                scenario_creator_kwargs={"branching_factors": a.bf, **AIRCOND_KW},
+                all_nodenames=create_nodenames_from_branching_factors(a.bf))
+        tag = f"aircond{a.scens}"
+        workload = f"aircond multistage PH (config 4), bf {'x'.join(map(str, a.bf))}"
     ph.PH_Prep()
     trivial_bound = ph.Iter0()
     e = ph.engine
@@ -200,7 +229,7 @@ def main():
     else:
         kname = "k_solve"
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_summary_farmer{a.scens}_cm{a.cm}.json")
+    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_summary_{tag}.json")
     if world == 1 and os.path.exists(pmc):
         try:
             d = json.load(open(pmc))
@@ -213,7 +242,7 @@ def main():
     # issue-side counters of the same kernel (rocprofv3 SQ_* passes, profiles/r01): what
     # actually bounds it, since the iterate never streams through HBM
     issue = None
-    sq = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_summary_farmer{a.scens}_cm{a.cm}.json")
+    sq = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_summary_{tag}.json")
     if world == 1 and os.path.exists(sq):
         try:
             d = json.load(open(sq))
@@ -246,8 +275,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (farmer scenario generator, seeded as farmer.py:52-60)",
-            "config": {"workload": "farmer PH (config 3)", "scenarios": a.scens, "crops_multiplier": a.cm,
+            "data": (f"synthetic ({a.model} scenario generator, seeded as "
+                     f"{'farmer.py:52-60' if a.model == 'farmer' else 'aircond.py:37-67'})"),
+            "config": {"workload": workload, "scenarios": a.scens,
+                       "crops_multiplier": a.cm if a.model == "farmer" else None,
+                       "tree_nodes": len(b.node_names),
                        "rho": a.rho, "eps_rel": a.eps, "scenarios_per_gpu": b.S,
                        "n": n, "m": m, "nnz": nnz, "parallelism": f"scenario-sharded x{world} (RCCL x̄ all-reduce)"},
             "solves_per_sec": ph_its * a.scens,

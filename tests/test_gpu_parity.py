@@ -103,6 +103,9 @@ def test_farmer_cm10_parity(gpu):
     ph = _ph(names, farmer.scenario_creator, {"crops_multiplier": 10, "num_scens": 16},
              batch_creator=farmer.batch_creator)
     conv, eobj, tb = ph.ph_main()
+    # the acreage row has 30 entries: served by a wide-row register instance at L = 64
+    info = ph.engine.kernel_info()
+    assert info["instance"] >= 0 and info["lanes"] == 64 and info["ZR"] >= 30, info
     assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
     assert (ph.engine.host("status") == 0).all()
     assert np.abs(ph.W_array() - np.array(g["W5"])).max() <= ABS
@@ -288,3 +291,33 @@ def test_gamma_not_one_uses_global_kernel(gpu):
     with pytest.raises(_lib.PhgpuError):
         e.solve(_lib.default_options(kernel=2, gamma=0.5), warm=False)
     e.close()
+
+
+def test_multinode_xbar_reduction_large_tree(gpu):
+    """Compute_Xbar (phbase.py:27-87) on a 3-level aircond tree large enough that node
+    runs span several waves and several merge chunks (bf 8 x 32 x 128: 32,768 scenarios,
+    512 waves, 264 non-leaf nodes): per-node x̄ equals the host sum of prob_coeff * x,
+    and two launches agree bit for bit."""
+    from mpisppy_amd.examples import aircond
+    from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+    bf = [8, 32, 128]
+    kw = dict(GOLD["aircond432_rho1"]["kwargs"])
+    kw["branching_factors"] = bf
+    names = aircond.scenario_names_creator(int(np.prod(bf)))
+    ph = _ph(names, aircond.scenario_creator, kw, iters=1, batch_creator=aircond.batch_creator,
+             all_nodenames=create_nodenames_from_branching_factors(bf))
+    ph.PH_Prep()
+    ph.Iter0()
+    ph.Compute_Xbar()
+    got = ph.xbar_by_node()
+    ph.Compute_Xbar()
+    again = ph.xbar_by_node()
+    b = ph.batch
+    X = ph.nonants_array()
+    exp = np.zeros((len(b.node_names), b.nlen_max))
+    for k in range(b.nn):
+        d, off = b.nonant_depth[k], b.nonant_off[k]
+        np.add.at(exp[:, off], b.node_of[:, d], b.prob_coeff[:, d] * X[:, k])
+    for g, nd in enumerate(b.node_names):
+        assert np.array_equal(got[nd], again[nd]), nd
+        assert np.allclose(got[nd], exp[g], rtol=1e-12, atol=1e-9), (nd, got[nd], exp[g])
