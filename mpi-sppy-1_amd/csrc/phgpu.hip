@@ -403,7 +403,9 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             ddx = sqrt(ddx);
             ddy = sqrt(ddy);
             if (ddx > 1e-10 && ddy > 1e-10)
-                omega = clampd(exp(0.5 * log(ddy / ddx) + 0.5 * log(omega)), P.wmin, P.wmax);
+                // geometric mean of omega and ||dy|| / ||dx||: exp(0.5 log(ddy/ddx) + 0.5 log(omega))
+                // as one sqrt (fp64 exp / log are long software sequences)
+                omega = clampd(sqrt(omega * (ddy / ddx)), P.wmin, P.wmax);
             hk = 0;
             r0 = -1.0;
             rlast = INFINITY;
