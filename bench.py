@@ -1,20 +1,27 @@
 """PH throughput benchmark (BASELINE.json metric): farmer, 65,536 scenarios, 1-8 GPUs.
 
-One "step" = one PH iteration of PHBase.iterk_loop (phbase.py:901-957):
-Compute_Xbar (kernel + RCCL all-reduce) -> Update_W + convergence_diff (kernel +
-all-reduce) -> solve_loop (one batched PDHG solve over the rank's scenarios).
-Model generation, Iter0 and the warmup iterations are outside the timed region.
+One "step" = one PH iteration of the product loop PHBase.iterk_loop (phbase.py:901-957):
+Compute_Xbar (kernels + all-reduce of the node buffer) -> Update_W + convergence_diff
+(kernel + scalar all-reduce, host readback of conv) -> solve_loop (one batched PDHG solve
+over the rank's scenarios, gripe status check).  The timed region is ``iterk_loop``
+itself, run for exactly K iterations.  Model generation, Iter0 and the W warmup
+iterations are outside it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm CM]
-    python bench.py --model aircond --bf 32,32,64     # config 4 (multistage), not the headline
+    python bench.py --model aircond --bf 32,32,64     # config 4 (multistage)
 
-N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL); scenarios are
-sharded contiguously (sputils.py:798-810); total scenarios are fixed (strong scaling).
-Rank 0 prints ONE JSON line.
+--gpus N > 1 started without torch.distributed.run launches itself with N local ranks
+(one per GPU, RCCL).  ``--backend gloo`` lets several ranks share one GPU (a functional
+rehearsal on a 1-GPU box; the x̄ all-reduce then goes through host memory).  Scenarios
+are sharded contiguously (sputils.py:798-810); the total is fixed (strong scaling).
+Rank 0 prints ONE JSON line on stdout (everything else goes to stderr).
 """
 import argparse
+import contextlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,14 +35,16 @@ METRIC = "PH iterations/sec + scenario subproblem solves/sec, farmer 64K scen, 1
 # config 4 parameters (straight_tests.py:36)
 AIRCOND_KW = {"Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50, "mu_dev": 0, "sigma_dev": 40,
               "start_seed": 0}
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_PEAK_TFLOPS = 78.6   # MI355X spec: fp64 vector = 1/2 of the 157.3 TF fp32 vector peak
+INFINITY_CACHE = 256 << 20
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--scens", type=int, default=65536)
     p.add_argument("--cm", type=int, default=1)
     p.add_argument("--model", choices=["farmer", "aircond"], default="farmer",
@@ -44,114 +53,235 @@ def parse():
                    help="aircond branching factors (scenarios = their product)")
     p.add_argument("--rho", type=float, default=1.0)
     p.add_argument("--eps", type=float, default=1e-9)
+    p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                   help="torch.distributed backend for N > 1 (auto: RCCL when every rank has its own GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
+    p.add_argument("--profile-dir", default=None,
+                   help="profiles/<round> directory holding the PMC summaries (default: newest)")
     return p.parse_args()
 
 
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------- self-launch
+def launch_ranks(a):
+    """--gpus N without a torch.distributed.run parent: start one (127.0.0.1 rendezvous)
+    as a child process -- nothing here has touched the GPU -- and exit with its code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    log("launching:", " ".join(cmd))
+    return subprocess.run(cmd, env=env).returncode
+
+
 # ---------------------------------------------------------------- CPU baseline
+_MODELS = {}
+
+
 def _cpu_worker(args):
-    """One worker = one rank of the reference's loop: its scenarios solved one at a time
-    by the oracle's exact per-scenario QP solver (spopt.py:284-294 structure)."""
-    names, cm, W, xbar, rho, S_total = args
+    """One worker = one rank of the reference's solve loop (spopt.py:284-294): its
+    scenarios solved one at a time, Iter0 LPs by HiGHS, PH QPs by the oracle's dense IPM
+    (stand-ins for the external LP/QP solver the reference calls per scenario)."""
+    names, cm, S_total, W, xbar, rho, iter0 = args
     import warnings
     warnings.simplefilter("ignore")
-    import numpy as np
     from oracle.models import farmer_scenario
-    from oracle.lpqp import solve_qp_ipm
+    from oracle.lpqp import solve_qp_ipm, solve_lp_highs
     xs = []
     for k, nm in enumerate(names):
-        s = farmer_scenario(nm, cm, num_scens=S_total)
-        A, rl, ru, lb, ub, c, q = s.arrays()
-        idx = s.nonant_indices()
-        c = c.copy()
-        q = q.copy()
-        c[idx] += W[k] - rho * xbar
-        q[idx] += rho
-        x, obj, st = solve_qp_ipm(A, rl, ru, lb, ub, c, q)
+        if nm not in _MODELS:
+            s = farmer_scenario(nm, cm, num_scens=S_total)
+            _MODELS[nm] = (s.arrays(), s.nonant_indices())
+        (A, rl, ru, lb, ub, c, q), idx = _MODELS[nm]
+        if iter0:
+            x, obj, st = solve_lp_highs(A, rl, ru, lb, ub, c)
+        else:
+            c = c.copy()
+            q = q.copy()
+            c[idx] += W[k] - rho * xbar
+            q[idx] += rho
+            x, obj, st = solve_qp_ipm(A, rl, ru, lb, ub, c, q)
         xs.append(x[idx])
     return np.array(xs)
 
 
-def cpu_baseline(S_total, cm, rho, sample):
-    """Time PH iterations of the CPU restatement on a bounded sample of the same farmer
-    workload, P = min(16, available cores) worker processes (spawned, no GPU state),
-    contiguous slices; extrapolate linearly in scenarios to S_total."""
+def _host_cpu():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return model, os.cpu_count(), aff
+
+
+def cpu_baseline(S_total, cm, rho, sample, iters=4):
+    """PH iterations of the CPU restatement on a bounded sample of the same workload.
+
+    P worker processes (spawned, no GPU state), one per host core this process may use
+    (the affinity set, capped by OMP_NUM_THREADS -- the box's CPU share); contiguous
+    slices (sputils.py:798-810); Iter0 (LP) then ``iters`` PH iterations with the real PH
+    state of the sample (x̄ -> W -> solve); per-iteration time = median of iterations
+    2..iters, scaled linearly to S_total scenarios."""
     import multiprocessing as mp
-    import numpy as np
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    P = max(1, min(16, cores))
+    model, ncpu, aff = _host_cpu()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    P = max(1, min(aff, share) if share > 0 else aff)
     names = [f"scen{i}" for i in range(sample)]
     nn = 3 * cm
-    rng = np.random.default_rng(0)
-    xbar = np.full(nn, 500.0 * cm / (3 * cm)) * rng.uniform(0.5, 1.0, nn)
-    W = rng.normal(0.0, 20.0, (sample, nn))
     avg = sample / P
     slices = [list(range(int(i * avg), int((i + 1) * avg))) for i in range(P)]
-    jobs = [([names[i] for i in sl], cm, W[sl], xbar, rho, S_total) for sl in slices if sl]
+    slices = [sl for sl in slices if sl]
+    W = np.zeros((sample, nn))
+    xbar = np.zeros(nn)
     ctx = mp.get_context("spawn")
     times = []
-    with ctx.Pool(len(jobs)) as pool:
-        pool.map(_cpu_worker, [(j[0][:1],) + j[1:] for j in jobs])  # warm the workers
-        for _ in range(2):
+    t_start = time.perf_counter()
+    with ctx.Pool(len(slices)) as pool:
+        def run(iter0):
+            out = pool.map(_cpu_worker, [([names[i] for i in sl], cm, S_total, W[sl], xbar, rho, iter0)
+                                         for sl in slices])
+            return np.concatenate(out)
+        x = run(True)                                  # Iter0 (builds and caches the models)
+        for _ in range(iters):
             t0 = time.perf_counter()
-            out = pool.map(_cpu_worker, jobs)
-            x = np.concatenate(out)
-            xb = x.mean(0)                         # Compute_Xbar + Update_W + conv
-            W = W + rho * (x - xb)
-            _ = np.abs(x - xb).mean()
+            xbar = x.mean(0)                           # Compute_Xbar (uniform p on the sample)
+            W = W + rho * (x - xbar)                   # Update_W
+            _ = np.abs(x - xbar).mean()                # convergence_diff
+            x = run(False)                             # solve_loop
             times.append(time.perf_counter() - t0)
-    t_it = float(np.median(times))
-    it_s_full = 1.0 / (t_it * (S_total / sample))
-    return {"value": it_s_full, "unit": "PH iterations/s", "cores": len(jobs), "kind": "port",
-            "sample": (f"farmer cm={cm}: {sample} of {S_total} scenarios, 2 PH iterations (QP solves "
-                       f"by the oracle's dense IPM, one scenario at a time per worker, {len(jobs)} "
-                       f"spawned workers); per-iteration time {t_it:.3f}s scaled x{S_total / sample:.0f} "
-                       f"to {S_total} scenarios"),
-            "sample_seconds_per_iteration": t_it}
+    t_it = float(np.median(times[1:]))
+    return {"value": 1.0 / (t_it * (S_total / sample)), "unit": "PH iterations/s", "cores": len(slices),
+            "kind": "port", "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "sample": (f"farmer cm={cm}: {sample} of {S_total} scenarios; Iter0 (HiGHS LP) + {iters} PH "
+                       f"iterations (QPs by the oracle's dense IPM, one scenario at a time per worker, "
+                       f"{len(slices)} spawned workers = the process's CPU share); median per-iteration "
+                       f"time of iterations 2..{iters} = {t_it:.3f}s, scaled x{S_total / sample:g} to "
+                       f"{S_total} scenarios"),
+            "sample_seconds_per_iteration": t_it, "wall_seconds": time.perf_counter() - t_start}
+
+
+# ---------------------------------------------------------------- roofline
+def _latest_profile_file(name, pdir=None):
+    dirs = [pdir] if pdir else sorted((d for d in os.listdir(os.path.join(ROOT, "profiles"))
+                                       if d.startswith("r")), reverse=True)
+    for d in dirs:
+        p = os.path.join(ROOT, "profiles", d, name)
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
+    """Roofline of the solve kernel.
+
+    The register-resident kernels keep each scenario's iterate in VGPRs / LDS for the
+    whole solve, so the binding resource is fp64 issue / latency: ``achieved`` =
+    algorithmic fp64 flops per launch (F = 4 nnz + 10 n + 6 m per scenario-iteration,
+    SURVEY.md 8(d)) / mean launch time, against the 78.6 TF fp64 vector peak.  The HBM
+    side is reported from measured PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE, gfx950
+    correction of MI355X_MICROARCH.md) of the same kernel, not from the per-iteration
+    byte model, which would exceed the 8 TB/s peak for an on-chip iterate."""
+    n, m, nnz, nn = b.n, b.m, b.nnz, b.nn
+    if kinfo["instance"] >= 0:
+        kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}>"
+    elif kinfo.get("wg", 0) > 0:
+        kname = "k_solve_wg"
+    else:
+        kname = "k_solve"
+    launch_ms = float(np.mean([t for t, _ in launches]))
+    units = float(np.mean([u for _, u in launches]))
+    F = 4 * nnz + 10 * n + 6 * m
+    B = 8 * (nnz + 5 * n + 4 * m + 3 * nn)
+    tflops = F * units / (launch_ms * 1e-3) / 1e12
+    traffic, src = None, None
+    pmc = _latest_profile_file(f"pmc_summary_{tag}.json", pdir)
+    if pmc:
+        try:
+            d = json.load(open(pmc))
+            tr = d.get("solve_traffic_bytes_per_launch", {}).get("void " + kname)
+            if tr is not None:
+                traffic = tr["total_upper"]
+                src = os.path.relpath(pmc, ROOT)
+        except Exception:
+            traffic = None
+    hbm_gbs = traffic / (launch_ms * 1e-3) / 1e9 if traffic else None
+    out = {"bound": "fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": src,
+           "hbm": {"achieved_GBs": hbm_gbs, "peak_GBs": HBM_PEAK_GBS,
+                   "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
+                   "note": "measured PMC bytes per launch (profiles/) / HIP-event launch time"},
+           "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
+           "kernel": kname, "lanes_per_scenario": kinfo["lanes"], "launch_ms": launch_ms,
+           "scenario_iters_per_launch": units, "flops_per_scenario_iter": F,
+           "model_bytes_per_scenario_iter": B,
+           "model_GBs_if_streamed": B * units / (launch_ms * 1e-3) / 1e9,
+           "note": ("achieved = F x scenario-iterations per launch / mean HIP-event launch time over the "
+                    "timed steps; F = 4nnz + 10n + 6m; bound fp64 because the iterate never leaves "
+                    "VGPRs/LDS (model_GBs_if_streamed, the SURVEY 8(d) byte model, exceeds HBM peak)")}
+    return out
 
 
 # ---------------------------------------------------------------- GPU run
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if a.gpus > 1 and world == 1:
-            raise SystemExit("for --gpus N > 1 launch with: python -m torch.distributed.run "
-                             "--nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N")
-    cpu = None
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     if a.model == "aircond":
         a.bf = [int(v) for v in a.bf.split(",")]
         a.scens = int(np.prod(a.bf))
+    cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.model == "farmer":
-        sample = a.cpu_sample or min(a.scens, 1024)
+        sample = a.cpu_sample or min(a.scens, 4096 if a.cm == 1 else 256)
         cpu = cpu_baseline(a.scens, a.cm, a.rho, sample)
+        log("cpu baseline:", json.dumps(cpu))
 
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
-    # several ranks may share one GPU in the gloo rehearsal (PHGPU_DIST_BACKEND=gloo)
-    local_rank = local_rank % max(1, ndev)
-    torch.cuda.set_device(local_rank)
+    backend = a.backend
+    if world > 1:
+        if backend == "auto":
+            backend = os.environ.get("PHGPU_DIST_BACKEND", "nccl" if ndev >= world else "")
+            if not backend:
+                raise SystemExit(f"{world} ranks but {ndev} visible GPU(s): use --backend gloo to "
+                                 f"rehearse with ranks sharing a GPU")
+        if backend == "nccl" and ndev < world:
+            raise SystemExit(f"RCCL needs one GPU per rank ({world} ranks, {ndev} GPUs)")
+    dev_index = local_rank % max(1, ndev)
+    torch.cuda.set_device(dev_index)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        # RCCL ("nccl") by default; PHGPU_DIST_BACKEND=gloo lets several ranks share one
-        # GPU (functional rehearsal of the multi-rank path on a 1-GPU box)
-        backend = os.environ.get("PHGPU_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group("gloo")
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     from mpisppy_amd.comm import Comm
 
     comm = Comm()
-    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 1, "defaultPHrho": a.rho, "convthresh": -1.0,
-            "verbose": False, "display_progress": False, "toc": False,
-            "device": f"cuda:{local_rank}",
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": a.warmup, "defaultPHrho": a.rho,
+            "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
+            "device": f"cuda:{dev_index}",
             "iter0_solver_options": {"eps_rel": a.eps}, "iterk_solver_options": {"eps_rel": a.eps}}
     t_setup = time.perf_counter()
     if a.model == "farmer":
@@ -163,8 +293,8 @@ def main():
         workload = {(65536, 1): "farmer PH (config 3)",
                     (1024, 10): "farmer PH (config 2)"}.get((a.scens, a.cm), f"farmer PH, cm={a.cm}")
     else:
-        # config 4: aircond multistage (aircond.py:37-330), default parameters, one
-        # scenario per leaf of the bf tree; per-node x̄ over all non-leaf nodes
+        # config 4: aircond multistage (aircond.py:37-330), one scenario per leaf of the bf
+        # tree; per-node x̄ over all non-leaf nodes
         from mpisppy_amd.examples import aircond
         from mpisppy_amd.sputils import create_nodenames_from_branching_factors
         names = aircond.scenario_names_creator(a.scens)
@@ -174,94 +304,35 @@ def main():
                 all_nodenames=create_nodenames_from_branching_factors(a.bf))
         tag = f"aircond{a.scens}"
         workload = f"aircond multistage PH (config 4), bf {'x'.join(map(str, a.bf))}"
-    ph.PH_Prep()
-    trivial_bound = ph.Iter0()
-    e = ph.engine
-    b = ph.batch
-    torch.cuda.synchronize()
-    t_setup = time.perf_counter() - t_setup
-
-    solve_ms = []
-    pdhg_iters = []
-    red_ms = []
-
-    # per-launch scenario-iterations for the roofline: a D2D snapshot of the iteration
-    # counts per step (one copy, no reduction kernel inside the timed region)
-    it_snap = torch.empty((a.warmup + a.steps, b.S), dtype=e.iters.dtype, device=e.device)
-
-    def step(k):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        ev[0].record()
-        ph.Compute_Xbar()
-        ph.Update_W()
-        conv = ph.convergence_diff()          # host sync (the reference's break test)
-        ev[1].record()
-        ph.solve_loop(solver_options=ph.current_solver_options)
-        ev[2].record()
-        it_snap[k].copy_(ph.engine.iters)
-        return ev, conv
-
-    for k in range(a.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    comm.Barrier()
-    t0 = time.perf_counter()
-    evs = []
-    for k in range(a.steps):
-        evs.append(step(a.warmup + k))
-    torch.cuda.synchronize()
-    comm.Barrier()
-    elapsed = time.perf_counter() - t0
-    units_per_step = it_snap[a.warmup:].sum(dim=1, dtype=torch.int64).cpu().tolist()
-    for (ev, conv) in evs:
-        red_ms.append(ev[0].elapsed_time(ev[1]))
-        solve_ms.append(ev[1].elapsed_time(ev[2]))
+    with contextlib.redirect_stdout(sys.stderr):
+        ph.PH_Prep()
+        trivial_bound = ph.Iter0()
+        e = ph.engine
+        b = ph.batch
+        ph.iterk_loop()                                # W warmup iterations (untimed)
+        torch.cuda.synchronize()
+        t_setup = time.perf_counter() - t_setup
+        e.instrument(a.steps)
+        ph.options["PHIterLimit"] = a.steps
+        comm.Barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ph.iterk_loop()                                # the product loop, K iterations
+        torch.cuda.synchronize()
+        comm.Barrier()
+        elapsed = time.perf_counter() - t0
+    launches = e.instrumented()
+    assert len(launches) == a.steps, (len(launches), a.steps)
     it_host = e.iters.cpu().numpy()
-    pdhg_iters = (int(it_host.max()), float(it_host.mean()))
     t = torch.tensor([elapsed], dtype=torch.float64, device=e.device)
     comm.allreduce_max_(t)
     elapsed = float(t.item())
-    # roofline of the dominant kernel (the batched solve): algorithmic bytes per launch
-    n, m, nnz, nn = b.n, b.m, b.nnz, b.nn
+    n_bad = torch.tensor([e.count_not_optimal()], dtype=torch.float64, device=e.device)
+    comm.allreduce_sum_(n_bad)
     kinfo = e.kernel_info()
-    if kinfo["instance"] >= 0:
-        kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}>"
-    else:
-        kname = "k_solve"
-    traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_summary_{tag}.json")
-    if world == 1 and os.path.exists(pmc):
-        try:
-            d = json.load(open(pmc))
-            tr = d.get("solve_traffic_bytes_per_launch", {}).get("void " + kname)
-            if tr is not None:
-                traffic = tr["total_upper"]
-                traffic_src = os.path.relpath(pmc, ROOT)
-        except Exception:
-            traffic = None
-    # issue-side counters of the same kernel (rocprofv3 SQ_* passes, profiles/r01): what
-    # actually bounds it, since the iterate never streams through HBM
-    issue = None
-    sq = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_summary_{tag}.json")
-    if world == 1 and os.path.exists(sq):
-        try:
-            d = json.load(open(sq))
-            if d.get("kernel") == "void " + kname:
-                dv = d["derived"]
-                issue = {"valu_busy": dv["valu_busy"], "lds_issue_busy": dv["lds_issue_busy"],
-                         "mean_waves_per_simd": dv["mean_waves_per_simd"],
-                         "fp64_tflops": dv["fp64_tflops"], "fp64_frac_of_vector_peak": dv["fp64_frac_of_peak"],
-                         "source": os.path.relpath(sq, ROOT)}
-        except Exception:
-            issue = None
-    B = 8 * (nnz + 5 * n + 4 * m + 3 * nn)           # SURVEY.md 8(d), per PDHG iter per scenario
-    # average over the K timed launches (HIP events on the launch stream); the rocprofv3
-    # kernel trace of the same command gives the per-dispatch durations (profiles/)
-    units = float(np.mean(units_per_step))           # scenario-iterations per launch
-    solve_s = float(np.mean(solve_ms)) / 1e3
-    achieved = B * units / solve_s / 1e9
+    ws = e.workspace_bytes() + 8 * (b.S * (b.n + b.m + 3 * max(b.nn, 1) + 4))
+    rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir)
     ph_its = a.steps / elapsed
-    status_ok = bool((e.status.cpu().numpy() == 0).all())
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -281,23 +352,19 @@ def main():
                        "crops_multiplier": a.cm if a.model == "farmer" else None,
                        "tree_nodes": len(b.node_names),
                        "rho": a.rho, "eps_rel": a.eps, "scenarios_per_gpu": b.S,
-                       "n": n, "m": m, "nnz": nnz, "parallelism": f"scenario-sharded x{world} (RCCL x̄ all-reduce)"},
+                       "n": b.n, "m": b.m, "nnz": b.nnz,
+                       "parallelism": (f"scenario-sharded x{world}" +
+                                       (f" ({'RCCL' if backend == 'nccl' else 'gloo, ranks sharing a GPU'}"
+                                        f" x̄ all-reduce)" if world > 1 else ""))},
             "solves_per_sec": ph_its * a.scens,
-            "pdhg_iters_per_ph_iter": {"max": pdhg_iters[0], "mean": pdhg_iters[1]},
-            "time_split_ms": {"solve": float(np.mean(solve_ms)), "xbar_W_conv": float(np.mean(red_ms))},
-            "all_optimal": status_ok,
+            "pdhg_iters_per_ph_iter": {"max": int(it_host.max()), "mean": float(it_host.mean())},
+            "time_split_ms": {"solve_launch": rl["launch_ms"],
+                              "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"]},
+            "timed_region": "PHBase.iterk_loop (x̄, W, conv readback, solve_loop with gripe)",
+            "all_optimal": bool(n_bad.item() == 0),
             "trivial_bound": trivial_bound,
             "setup_s": t_setup,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src, "issue": issue,
-                         "kernel": kname, "lanes_per_scenario": kinfo["lanes"],
-                         "bytes_per_scenario_iter": B,
-                         "scenario_iters_per_launch": units, "launch_ms": solve_s * 1e3,
-                         "note": ("achieved = algorithmic PDHG bytes (SURVEY.md 8(d): 8*(nnz+5n+4m+3nn) per "
-                                  "scenario-iteration) / launch time; the register-resident kernel keeps the "
-                                  "iterates in VGPRs/LDS, so measured HBM traffic per launch (PMC FETCH_SIZE*2 + "
-                                  "WRITE_SIZE) is far below it")},
+            "roofline": rl,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

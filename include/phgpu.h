@@ -47,7 +47,9 @@ extern "C" {
 typedef struct phgpu_state* phgpu_handle;
 
 /* Per-scenario solve status (mapped to _mpisppy_data.scenario_feasible and the
- * termination_condition checks of spopt.py:175-194). */
+ * termination_condition checks of spopt.py:175-194).  PRIMAL_INFEASIBLE: a dual ray
+ * (Farkas certificate) was found, obj = bound = +inf; DUAL_INFEASIBLE: a primal ray of
+ * descent was found (the subproblem is unbounded), obj = bound = -inf. */
 enum {
     PHGPU_OPTIMAL = 0,
     PHGPU_ITER_LIMIT = 1,
@@ -74,9 +76,16 @@ typedef struct {
                               of all iterations of the solve                  [0.36] */
     double omega_clamp;    /* primal weight kept in [1/clamp, clamp] (scaled) [1e4] */
     int32_t kernel;        /* 0 auto, 1 global-memory kernel, 2 register-resident
-                              kernel (error if no compiled instance fits)      [0] */
-    int32_t reserved;
+                              kernel (error if no compiled instance fits),
+                              3 workgroup-per-scenario kernel (large scenarios) [0] */
+    int32_t infeas_start;  /* infeasibility certificates are tested at the KKT
+                              checks from this iteration on (< 0: never)      [512] */
+    double eps_infeas;     /* certificate tolerance: ray violation <= eps * |ray
+                              objective| (PDLP-style)      [1e-8] */
 } phgpu_options;
+/* max_iter must be a multiple of restart_every: the register-resident kernel counts
+ * iterations in chunks of restart_every and stops exactly at max_iter (both kernels then
+ * report iters == max_iter on ITER_LIMIT). */
 
 /* Fill *opt with the defaults shown above. */
 int phgpu_default_options(phgpu_options* opt);

@@ -121,6 +121,47 @@ __device__ __forceinline__ double col_dual_term(double r, double qq, double lb, 
     return 0.0;
 }
 
+// ---------------------------------------------------------- infeasibility certificates
+// PDLP-style tests on the fixed-point residual d = T(z) - z, which for an infeasible or
+// unbounded problem converges to the minimal displacement of the PDHG operator (its dual
+// part is a Farkas ray, its primal part a ray of descent).  All quantities are in the
+// original space.  The reference marks such a scenario infeasible (spopt.py:175-194) and
+// Iter0 stops on it (phbase.py:818-823).
+//
+// Primal infeasibility: dual ray d (rows), ray reduced cost r = -(A^T d) (columns).  The
+// ray objective sum_i min_{s in [rl,ru]} s d_i + sum_j min_{x in [lb,ub]} r_j x_j must be
+// > 0 while every component that points at an infinite side (where the min is -inf) is
+// ~0: certificate if sqrt(viol2) <= eps * obj.
+__device__ __forceinline__ void ray_row_terms(double d, double rl, double ru, double& obj, double& viol2) {
+    if (d > 0.0) {
+        if (isfinite(rl)) obj += rl * d;
+        else viol2 += d * d;
+    } else if (d < 0.0) {
+        if (isfinite(ru)) obj += ru * d;
+        else viol2 += d * d;
+    }
+}
+__device__ __forceinline__ void ray_col_terms(double r, double lb, double ub, double& obj, double& viol2) {
+    if (r > 0.0) {
+        if (isfinite(lb)) obj += lb * r;
+        else viol2 += r * r;
+    } else if (r < 0.0) {
+        if (isfinite(ub)) obj += ub * r;
+        else viol2 += r * r;
+    }
+}
+// Dual infeasibility (unbounded primal): primal ray dx with c'dx < 0, Q dx = 0, A dx in
+// the recession cone of [rl, ru] and dx in that of [lb, ub]; squared distance to the cone.
+__device__ __forceinline__ double recession_viol2(double a, double lo, double hi) {
+    double v = 0.0;
+    if (isfinite(lo) && a < 0.0) v += a * a;
+    if (isfinite(hi) && a > 0.0) v += a * a;
+    return v;
+}
+__device__ __forceinline__ bool is_certificate(double obj, double viol2, double eps) {
+    return obj > 0.0 && viol2 <= (eps * obj) * (eps * obj);
+}
+
 // ------------------------------------------------------------------ setup kernel
 // Per scenario: copy A, Ruiz (iters) + Pock-Chambolle(alpha=1) scaling, scaled
 // bounds, CSC copy of the scaled values and ||A_scaled||_2 by power iteration.
@@ -205,8 +246,8 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
 
 // ------------------------------------------------------------------ solve kernel
 struct solve_params {
-    double eps_rel, eps_abs, gamma, bsuff, bnec, bart, eta_frac, omega0, wmin, wmax;
-    int max_iter, check_every, restart_every, warm, keep_omega;
+    double eps_rel, eps_abs, gamma, bsuff, bnec, bart, eta_frac, omega0, wmin, wmax, eps_inf;
+    int max_iter, check_every, restart_every, warm, keep_omega, infeas_start;
 };
 
 __global__ void __launch_bounds__(BLOCK)
@@ -356,7 +397,8 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             const double xo = d * xt[IX(j)];
             const double ce = ch[IX(j)] / d, qe = qh[IX(j)] / (d * d);
             const double at = xe[IX(j)] / d;
-            const double lbj = st.lb[IX(j)], ubj = st.ub[IX(j)];
+            // working bounds (phgpu_fix_nonants may have fixed this column)
+            const double lbj = st.lbh[IX(j)] * d, ubj = st.ubh[IX(j)] * d;
             const double rc = ce + qe * xo - at;
             double lam;
             if (isfinite(lbj) && isfinite(ubj)) lam = rc;
@@ -375,6 +417,37 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             stat = PHGPU_OPTIMAL;
             final_is_t = true;
             break;
+        }
+        if (P.infeas_start >= 0 && it >= P.infeas_start) {
+            // certificates from d = T(z) - z (x, y: the iterate; xt, yt: T(z); aty = A^T y,
+            // xe = A^T yt)
+            double pobj_r = 0.0, pviol = 0.0, cdx = 0.0, dviol = 0.0;
+            for (int i = 0; i < m; ++i) {
+                const double dr = st.Dr[IX(i)];
+                const double rl = st.rl[IX(i)], ru = st.ru[IX(i)];
+                ray_row_terms(dr * (yt[IX(i)] - y[IX(i)]), rl, ru, pobj_r, pviol);
+                double adx = 0.0;
+                for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k)
+                    adx += Ahr[IX(k)] * (xt[IX(col_idx[k])] - x[IX(col_idx[k])]);
+                dviol += recession_viol2(adx / dr, rl, ru);
+            }
+            for (int j = 0; j < n; ++j) {
+                const double d = st.Dc[IX(j)];
+                const double lbj = st.lbh[IX(j)] * d, ubj = st.ubh[IX(j)] * d;
+                ray_col_terms(-(xe[IX(j)] - aty[IX(j)]) / d, lbj, ubj, pobj_r, pviol);
+                const double dxo = d * (xt[IX(j)] - x[IX(j)]);
+                const double qe = qh[IX(j)] / (d * d);
+                cdx += (ch[IX(j)] / d) * dxo;
+                dviol += recession_viol2(dxo, lbj, ubj) + (qe * dxo) * (qe * dxo);
+            }
+            if (is_certificate(pobj_r, pviol, P.eps_inf)) {
+                stat = PHGPU_PRIMAL_INFEASIBLE;
+                break;
+            }
+            if (is_certificate(-cdx, dviol, P.eps_inf)) {
+                stat = PHGPU_DUAL_INFEASIBLE;
+                break;
+            }
         }
         }
         // ---- restart test (cuPDLP+-style: sufficient decay / necessary decay without
@@ -438,9 +511,11 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
             const double xo = d * x[IX(j)];
             const double ce = ch[IX(j)] / d, qe = qh[IX(j)] / (d * d);
             pobj += ce * xo + 0.5 * qe * xo * xo;
-            dobj += col_dual_term(ce - aty[IX(j)] / d, qe, st.lb[IX(j)], st.ub[IX(j)]);
+            dobj += col_dual_term(ce - aty[IX(j)] / d, qe, st.lbh[IX(j)] * d, st.ubh[IX(j)] * d);
         }
     }
+    if (stat == PHGPU_PRIMAL_INFEASIBLE) pobj = dobj = INFINITY;
+    if (stat == PHGPU_DUAL_INFEASIBLE) pobj = dobj = -INFINITY;
     for (int j = 0; j < n; ++j) xout[IX(j)] = st.Dc[IX(j)] * x[IX(j)];
     if (yout)
         for (int i = 0; i < m; ++i) yout[IX(i)] = st.Dr[IX(i)] * y[IX(i)];
@@ -448,7 +523,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     obj[s] = pobj;
     bound[s] = dobj;
     status[s] = stat;
-    if (iters) iters[s] = final_is_t ? it : P.max_iter;
+    if (iters) iters[s] = (stat == PHGPU_ITER_LIMIT) ? P.max_iter : it;
 }
 
 #include "solve_reg.inc"
@@ -801,6 +876,8 @@ extern "C" int phgpu_default_options(phgpu_options* o) {
     o->beta_artificial = 0.36;
     o->omega_clamp = 1e4;
     o->kernel = 0;
+    o->infeas_start = 512;
+    o->eps_infeas = 1e-8;
     return 0;
 }
 
@@ -1061,9 +1138,11 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     if (opt) o = *opt;
     else phgpu_default_options(&o);
     if (o.check_every < 1 || o.max_iter < 1 || !(o.eta_frac > 0.0 && o.eta_frac < 1.0) ||
-        o.gamma < 0.0 || o.gamma > 1.0 || o.restart_every < 1 || o.check_every % o.restart_every != 0)
-        return set_err(-1, "bad options (check_every=%d restart_every=%d max_iter=%d eta_frac=%g gamma=%g)",
-                       o.check_every, o.restart_every, o.max_iter, o.eta_frac, o.gamma);
+        o.gamma < 0.0 || o.gamma > 1.0 || o.restart_every < 1 || o.check_every % o.restart_every != 0 ||
+        o.max_iter % o.restart_every != 0 || !(o.eps_infeas > 0.0))
+        return set_err(-1, "bad options (check_every=%d restart_every=%d max_iter=%d eta_frac=%g gamma=%g "
+                       "eps_infeas=%g; check_every and max_iter must be multiples of restart_every)",
+                       o.check_every, o.restart_every, o.max_iter, o.eta_frac, o.gamma, o.eps_infeas);
     solve_params P;
     P.eps_rel = o.eps_rel;
     P.eps_abs = o.eps_abs;
@@ -1078,6 +1157,8 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     P.check_every = o.check_every;
     P.warm = (warm_start && h->have_solution) ? 1 : 0;
     P.keep_omega = o.keep_omega;
+    P.infeas_start = o.infeas_start;
+    P.eps_inf = o.eps_infeas;
     P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
     P.wmin = 1.0 / P.wmax;
     hipStream_t st = (hipStream_t)stream;

@@ -34,7 +34,8 @@ class PhgpuOptions(ctypes.Structure):
         ("beta_artificial", c_dbl),
         ("omega_clamp", c_dbl),
         ("kernel", c_i32),
-        ("reserved", c_i32),
+        ("infeas_start", c_i32),
+        ("eps_infeas", c_dbl),
     ]
 
 

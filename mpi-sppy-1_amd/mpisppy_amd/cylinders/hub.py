@@ -253,7 +253,9 @@ class PHHub(Hub):
 
     # hub.py:519-547
     def is_converged(self):
-        if self.opt._PHIter == 1:
+        # the trivial bound is a valid outer bound only when every Iter0 solve was certified
+        # optimal (an ITER_LIMIT dual bound may overstate it; see PHBase.Iter0)
+        if self.opt._PHIter == 1 and getattr(self.opt, "trivial_bound_certified", True):
             self.BestOuterBound = self.OuterBoundUpdate(self.opt.trivial_bound)
         if not self.has_innerbound_spokes:
             if self.opt._PHIter == 1:

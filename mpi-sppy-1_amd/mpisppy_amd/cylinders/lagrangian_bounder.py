@@ -25,7 +25,14 @@ class LagrangianOuterBound(OuterBoundWSpoke):
         verbose = self.opt.options["verbose"]
         self.opt.solve_loop(solver_options=self.opt.current_solver_options, dtiming=False, gripe=True,
                             verbose=verbose)
-        return self.opt.Ebound(verbose)
+        # only a fully certified solve gives a valid Lagrangian bound: a scenario at the
+        # iteration cap reports a dual objective that is not a bound, an infeasible one
+        # +-inf.  None keeps the previous bound (do_work), as a failed solve does in the
+        # reference (lagrangian_bounder.py:36-47)
+        Eobj, Ebound, E1, Efeas, Eopt = self.opt.engine.expectations()
+        if abs(Eopt - E1) > 1e-12 * max(1.0, abs(E1)):
+            return None
+        return self.opt.batch.sense * Ebound
 
     # lagrangian_bounder.py:58-60 (W_from_flat_list with the hub's W, device to device)
     def _set_weights_and_solve(self):
@@ -38,7 +45,8 @@ class LagrangianOuterBound(OuterBoundWSpoke):
         self.dk_iter = 1
         self.trivial_bound = self.lagrangian()
         self.opt.current_solver_options = self.opt.iterk_solver_options
-        self.bound = self.trivial_bound
+        if self.trivial_bound is not None:
+            self.bound = self.trivial_bound
 
     def do_work(self):
         if self.new_Ws:
@@ -51,9 +59,10 @@ class LagrangianOuterBound(OuterBoundWSpoke):
     # delivers them with the kill signal; without a new W the last bound stands)
     def finalize(self):
         self.got_kill_signal()
-        if self.new_Ws:
-            self.final_bound = self._set_weights_and_solve()
-            self.bound = self.final_bound
+        final = self._set_weights_and_solve() if self.new_Ws else None
+        if final is not None:
+            self.final_bound = final
+            self.bound = final
         else:
             self.final_bound = self.bound
         if self.opt.extensions is not None and hasattr(self.opt.extobject, "post_everything"):

@@ -157,13 +157,46 @@ class PHEngine:
         self.prox_on = 1 if prox_on else 0
         self._bind()
 
+    # -------------------------------------------------------------- instrumentation
+    def instrument(self, max_solves):
+        """Record the next ``max_solves`` phgpu_solve launches: HIP events on the launch
+        stream around each launch and a device snapshot of the per-scenario PDHG
+        iteration counts (one D2D copy after the launch, outside the event pair).  Used
+        by bench.py for the per-launch roofline inside its timed region."""
+        self._ins = {"events": [], "iters": torch.empty((max_solves, self.S), dtype=torch.int32,
+                                                         device=self.device)}
+
+    def instrumented(self):
+        """[(launch ms, scenario-iterations)] of the recorded launches (syncs)."""
+        ins = getattr(self, "_ins", None)
+        if not ins:
+            return []
+        torch.cuda.synchronize(self.device)
+        k = len(ins["events"])
+        its = ins["iters"][:k].sum(dim=1, dtype=torch.int64).cpu().tolist()
+        return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
+
     # -------------------------------------------------------------- hot path
     def solve(self, options=None, warm=True):
         o = options if options is not None else _lib.default_options()
+        ins = getattr(self, "_ins", None)
+        rec = ins is not None and len(ins["events"]) < ins["iters"].shape[0]
+        if rec:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(self.x),
                                         _ptr(self.y), _ptr(self.obj), _ptr(self.bound),
                                         _ptr(self.status), _ptr(self.iters), self._stream()),
                    "phgpu_solve")
+        if rec:
+            ev[1].record()
+            ins["iters"][len(ins["events"])].copy_(self.iters)
+            ins["events"].append(ev)
+
+    def count_not_optimal(self):
+        """Number of local scenarios whose last solve is not OPTIMAL (device count, one
+        scalar read back)."""
+        return int(torch.count_nonzero(self.status).item())
 
     def compute_xbar_partials(self):
         _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),

@@ -164,9 +164,19 @@ class PHBase(SPOpt):
             # the reference prints ERROR and calls quit() (phbase.py:812-817)
             raise RuntimeError(f"Total probability of scenarios was {self.E1} "
                                f"(E1_tolerance = {self.E1_tolerance})")
-        feasP = self.feas_prob()
+        _, _, _, feasP, optP = self.engine.expectations()
         if abs(feasP - self.E1) > 1e-12 * max(1.0, abs(self.E1)):
-            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1}")  # :818-823
+            # a PDHG infeasibility / unboundedness certificate (status 2 / 3); the reference
+            # prints the same message and quit()s (phbase.py:818-823)
+            raise RuntimeError(f"Infeasibility detected; E_feas, E1= {feasP} {self.E1}")
+        # scenarios at the PDHG iteration cap carry an approximate x and an uncertified
+        # bound: say so on every rank, and keep the trivial bound out of the hub's
+        # BestOuterBound (trivial_bound_certified)
+        self.trivial_bound_certified = abs(optP - self.E1) <= 1e-12 * max(1.0, abs(self.E1))
+        if not self.trivial_bound_certified:
+            print(f"WARNING (rank {self.cylinder_rank}): Iter0 solves at the PDHG iteration limit "
+                  f"carry probability {self.E1 - optP:.3g}; their x enters x̄ unconverged and the "
+                  f"trivial bound is not certified", flush=True)
         if self.extensions is not None and hasattr(self.extobject, "post_iter0"):
             self.extobject.post_iter0()
         if self.spcomm is not None:

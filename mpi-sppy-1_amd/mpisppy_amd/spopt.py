@@ -74,7 +74,7 @@ class SPOpt(SPBase):
         if dtiming and self.cylinder_rank == 0:
             print("Batched solve time (seconds): %4.4f  PDHG iters max/mean %d/%.1f"
                   % (self.solve_times[-1], *self.pdhg_iters[-1]))
-        if gripe:
+        if gripe and self.engine.count_not_optimal() > 0:
             st = self.engine.status.cpu().numpy()
             bad = np.nonzero((st != _lib.OPTIMAL) & (st != _lib.ITER_LIMIT))[0]
             for k in bad[:10]:

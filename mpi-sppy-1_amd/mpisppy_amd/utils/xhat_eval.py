@@ -8,9 +8,10 @@ objective (xhat_eval.py:212-291).  Here the fix is one kernel over all local sce
 the engine's deterministic tree sum.  The objective has no PH terms (W and prox are
 never attached to an Xhat_Eval, xhat_eval.py:29-60).
 
-A candidate is accepted only when every scenario solve is certified OPTIMAL: the
-engine has no infeasibility certificate yet, so ITER_LIMIT counts as infeasible here
-(stricter than feas_prob, which the hub uses for Iter0).
+A candidate is accepted only when every scenario solve is certified OPTIMAL: a fixing
+that makes a scenario infeasible is certified PRIMAL_INFEASIBLE by the engine, and a
+solve left at ITER_LIMIT counts as not accepted too (stricter than feas_prob, which
+counts ITER_LIMIT as a loaded solution).
 """
 import numpy as np
 import torch

@@ -1,0 +1,203 @@
+"""Vectorised exact farmer oracle for headline-scale parity (TEST INFRASTRUCTURE ONLY).
+
+The farmer scenario (examples/farmer/farmer.py:85-224) is separable per crop once the
+recourse variables are eliminated: crop k's first + second stage cost is a convex
+piecewise-linear function g_k(x_k) of its acreage, coupled only by the acreage row
+sum_k x_k <= 500 cm (farmer.py:181-184).  Per crop (farmer.py:186-222, data :127-150):
+
+  * WHEAT / CORN: buy the feed shortfall (req - Y x)+ at PurchasePrice, sell the surplus
+    at SubQuotaSellingPrice up to the 1e5 quota, then at SuperQuotaSellingPrice (0):
+    slopes  plant - buy Y | plant - sub Y | plant - super Y
+    kinks   req / Y       | (req + 1e5) / Y
+  * SUGAR_BEETS: sell up to the 6000 quota at 36, then at 10:
+    slopes  260 - 36 Y    | 260 - 10 Y
+    kinks   6000 / Y
+
+(The quota kink of WHEAT / CORN only matters once 500 cm acres of one crop can exceed
+it -- cm >= ~28, e.g. the cm = 64 variant of config 3.)
+
+Solvers, all vectorised over scenarios with numpy:
+
+  * ``iter0_lp``: the Iter0 LP (W_on = prox_on = 0, phbase.py:594-597): a fractional
+    knapsack -- the segments with negative slope are filled in slope order until the
+    acreage is used up (exact; unique x when no two slopes tie).
+  * ``prox``: the PH subproblem  min sum_k g_k(x_k) + W_k x_k + rho/2 (x_k - xbar_k)^2
+    s.t. sum x_k <= 500 cm (phbase.py:617-699): for a multiplier lam of the acreage row
+    each crop's minimiser is  b0 + sum_i clamp(xbar - (s_i + W + lam)/rho - b_{i-1}, 0,
+    b_i - b_{i-1}); lam >= 0 by bisection (the same closed form as lpqp.farmer_prox_exact,
+    which tests/test_oracle_golden.py pins against the reference's w_test_data).
+
+``FarmerVecPH`` restates PHBase.Iter0 / iterk_loop (phbase.py:758-979) for a
+single-rank run on these solvers.  It is checked against HiGHS (LP) and
+lpqp.farmer_prox_exact on samples in tests/test_oracle_scale.py.
+"""
+import math
+
+import numpy as np
+
+from .models import extract_num
+
+_PLANT = {"WHEAT": 150.0, "CORN": 230.0, "SUGAR_BEETS": 260.0}
+_REQ = {"WHEAT": 200.0, "CORN": 240.0}
+_BUY = {"WHEAT": 238.0, "CORN": 210.0}
+_SUB = {"WHEAT": 170.0, "CORN": 150.0, "SUGAR_BEETS": 36.0}
+_SUPER = {"WHEAT": 0.0, "CORN": 0.0, "SUGAR_BEETS": 10.0}
+_QUOTA = {"WHEAT": 100000.0, "CORN": 100000.0, "SUGAR_BEETS": 6000.0}
+_BASE_Y = [
+    {"WHEAT": 2.0, "CORN": 2.4, "SUGAR_BEETS": 16.0},   # BelowAverageScenario
+    {"WHEAT": 2.5, "CORN": 3.0, "SUGAR_BEETS": 20.0},   # AverageScenario
+    {"WHEAT": 3.0, "CORN": 3.6, "SUGAR_BEETS": 24.0},   # AboveAverageScenario
+]
+_BASES = ["WHEAT", "CORN", "SUGAR_BEETS"]
+
+
+def crops_insertion(cm):
+    """CROPS order (farmer.py:99-105)."""
+    return [b + str(i) for i in range(cm) for b in _BASES]
+
+
+def crops_sorted(cm):
+    """Nonant order: DevotedAcreage expanded in sorted key order (scenario_tree.py:39)."""
+    return sorted(crops_insertion(cm))
+
+
+def yields(names, cm, seedoffset=0):
+    """[S, 3cm] yields in CROPS order (farmer.py:52-60, 151-157)."""
+    out = np.empty((len(names), 3 * cm))
+    for s, nm in enumerate(names):
+        num = extract_num(nm)
+        base = _BASE_Y[num % 3]
+        y = np.array([base[b] for b in _BASES] * cm)
+        if num // 3 != 0:
+            st = np.random.RandomState()
+            st.seed(num + seedoffset)
+            y = y + st.rand(3 * cm)
+        out[s] = y
+    return out
+
+
+def pieces(Y, cm):
+    """Breakpoints [S, K, 4] and slopes [S, K, 3] of g_k on [0, 500 cm] plus g_k(0)
+    [S, K], in the SORTED nonant order (K = 3 cm)."""
+    total = 500.0 * cm
+    ins = crops_insertion(cm)
+    order = [ins.index(c) for c in crops_sorted(cm)]
+    Y = Y[:, order]
+    S, K = Y.shape
+    bases = [c.rstrip("0123456789") for c in crops_sorted(cm)]
+    bp = np.zeros((S, K, 4))
+    sl = np.zeros((S, K, 3))
+    f0 = np.zeros((S, K))
+    for k, b in enumerate(bases):
+        y = Y[:, k]
+        if b in ("WHEAT", "CORN"):
+            k1 = _REQ[b] / y
+            k2 = (_REQ[b] + _QUOTA[b]) / y
+            sl[:, k] = np.stack([_PLANT[b] - _BUY[b] * y, _PLANT[b] - _SUB[b] * y,
+                                 _PLANT[b] - _SUPER[b] * y], axis=1)
+            f0[:, k] = _BUY[b] * _REQ[b]
+        else:
+            k1 = _QUOTA[b] / y
+            k2 = np.full_like(y, np.inf)
+            sl[:, k] = np.stack([_PLANT[b] - _SUB[b] * y, _PLANT[b] - _SUPER[b] * y,
+                                 _PLANT[b] - _SUPER[b] * y], axis=1)
+        bp[:, k, 1] = np.minimum(k1, total)
+        bp[:, k, 2] = np.minimum(k2, total)
+        bp[:, k, 3] = total
+    return bp, sl, f0
+
+
+def crop_cost(bp, sl, f0, x):
+    """g_k(x_k), [S, K]."""
+    seg = np.clip(x[..., None] - bp[..., :-1], 0.0, np.diff(bp, axis=-1))
+    return f0 + (sl * seg).sum(-1)
+
+
+def iter0_lp(bp, sl, f0, total):
+    """Exact Iter0 LP: fractional knapsack over the negative-slope segments."""
+    S, K, J = sl.shape
+    length = np.diff(bp, axis=-1).reshape(S, K * J)
+    slope = sl.reshape(S, K * J)
+    order = np.argsort(slope, axis=1, kind="stable")
+    sl_o = np.take_along_axis(slope, order, 1)
+    len_o = np.where(sl_o < 0.0, np.take_along_axis(length, order, 1), 0.0)
+    before = np.cumsum(len_o, axis=1) - len_o
+    fill_o = np.clip(total - before, 0.0, len_o)
+    fill = np.empty_like(fill_o)
+    np.put_along_axis(fill, order, fill_o, 1)
+    x = fill.reshape(S, K, J).sum(-1)
+    obj = f0.sum(1) + (slope * fill).sum(1)
+    return x, obj
+
+
+def _x_of_lam(bp, sl, lin, rho, xbar, lam):
+    a = xbar[..., None] - (sl + (lin + lam[:, None])[..., None]) / rho[..., None]
+    return bp[..., 0] + np.clip(a - bp[..., :-1], 0.0, np.diff(bp, axis=-1)).sum(-1)
+
+
+def prox(bp, sl, f0, W, xbar, rho, total, iters=200):
+    """Exact PH subproblem for all scenarios: (x [S, K], augmented objective [S])."""
+    S = bp.shape[0]
+    lam = np.zeros(S)
+    x = _x_of_lam(bp, sl, W, rho, xbar, lam)
+    over = x.sum(1) > total
+    if over.any():
+        lo = np.zeros(S)
+        hi = np.ones(S)
+        while True:
+            bad = over & (_x_of_lam(bp, sl, W, rho, xbar, hi).sum(1) > total)
+            if not bad.any():
+                break
+            hi[bad] *= 2.0
+        for _ in range(iters):
+            mid = 0.5 * (lo + hi)
+            gt = _x_of_lam(bp, sl, W, rho, xbar, mid).sum(1) > total
+            lo = np.where(gt, mid, lo)
+            hi = np.where(gt, hi, mid)
+        xh = _x_of_lam(bp, sl, W, rho, xbar, hi)
+        x = np.where(over[:, None], xh, x)
+    obj = crop_cost(bp, sl, f0, x).sum(1) + (W * x).sum(1) + 0.5 * (rho * (x - xbar) ** 2).sum(1)
+    return x, obj
+
+
+class FarmerVecPH:
+    """Single-rank PH on the vectorised farmer solvers (phbase.py:758-979)."""
+
+    def __init__(self, names, cm, rho=1.0, num_scens=None, seedoffset=0):
+        self.names = list(names)
+        self.cm = cm
+        self.total = 500.0 * cm
+        self.S = len(self.names)
+        self.K = 3 * cm
+        self.prob = np.full(self.S, 1.0 / (num_scens or self.S))   # spbase.py:515-520
+        self.bp, self.sl, self.f0 = pieces(yields(self.names, cm, seedoffset), cm)
+        self.rho = np.full((self.S, self.K), float(rho))
+        self.W = np.zeros((self.S, self.K))
+        self.xbar = np.zeros((self.S, self.K))
+        self.history = []
+
+    def iter0(self):
+        self.x, self.obj = iter0_lp(self.bp, self.sl, self.f0, self.total)
+        self.iter0_x = self.x.copy()
+        self.iter0_obj = self.obj.copy()
+        self.trivial_bound = math.fsum(self.prob * self.obj)        # spopt.py:346-391
+        return self.trivial_bound
+
+    def compute_xbar(self):                                          # phbase.py:27-107
+        xb = (self.prob[:, None] * self.x).sum(0)              # prob_coeff = pi_s / pi_ROOT
+        self.xbar[:] = xb
+        return xb
+
+    def iterk_loop(self, max_iterations, convthresh=-1.0):
+        for it in range(1, max_iterations + 1):
+            xb = self.compute_xbar()
+            self.W += self.rho * (self.x - self.xbar)                # phbase.py:293-318
+            conv = np.abs(self.x - self.xbar).sum() / (self.S * self.K)   # :321-343
+            self.history.append({"iter": it, "conv": conv, "xbar": xb.copy()})
+            if conv < convthresh:
+                return it
+            self.x, self.obj = prox(self.bp, self.sl, self.f0, self.W, self.xbar, self.rho, self.total)
+        return max_iterations
+
+    def Eobjective(self):
+        return math.fsum(self.prob * self.obj)

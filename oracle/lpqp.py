@@ -193,8 +193,10 @@ def _farmer_crop_pieces(base, Y, cm):
     acreage x in [0, 500*cm]: returns (breakpoints, slopes, value at 0).
 
     Restates the recourse of farmer.py:181-222 for one crop: wheat/corn buy the feed
-    shortfall at PurchasePrice or sell the surplus at SubQuotaSellingPrice (quota
-    1e5 never binds); beets sell up to the 6000 quota at 36 and the rest at 10.
+    shortfall at PurchasePrice, sell the surplus at SubQuotaSellingPrice up to the 1e5
+    quota and the rest at SuperQuotaSellingPrice (0; the quota kink lies inside
+    [0, 500 cm] only for cm >= ~28); beets sell up to the 6000 quota at 36 and the rest
+    at 10.
     """
     total = 500.0 * cm
     plant = {"WHEAT": 150.0, "CORN": 230.0, "SUGAR_BEETS": 260.0}[base]
@@ -203,8 +205,10 @@ def _farmer_crop_pieces(base, Y, cm):
         buy = {"WHEAT": 238.0, "CORN": 210.0}[base]
         sub = {"WHEAT": 170.0, "CORN": 150.0}[base]
         kink = req / Y
+        kq = (req + 100000.0) / Y
         f0 = buy * req
-        return [0.0, min(kink, total), total], [plant - buy * Y, plant - sub * Y], f0
+        return ([0.0, min(kink, total), min(kq, total), total],
+                [plant - buy * Y, plant - sub * Y, plant], f0)
     kink = 6000.0 / Y
     return [0.0, min(kink, total), total], [plant - 36.0 * Y, plant - 10.0 * Y], 0.0
 

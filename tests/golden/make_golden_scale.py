@@ -1,0 +1,64 @@
+"""Generate the configuration-scale farmer fixtures (tests/golden/farmer_scale.json).
+
+Run:  python tests/golden/make_golden_scale.py        (~1 minute, one core)
+
+Source: oracle/farmer_vec.py, the vectorised exact restatement of farmer.py:85-224 and
+PHBase.Iter0 / iterk_loop (phbase.py:758-979).  It is pinned by tests/test_oracle_scale.py:
+its Iter0 LP matches scipy's HiGHS and its PH subproblem matches lpqp.farmer_prox_exact
+(which reproduces the reference's w_test_data fixtures) on samples of every set below.
+
+Sets (SURVEY.md 8(c) "golden vectors to commit"):
+  farmer65536_cm1   config 3: scen0..scen65535, cm=1, rho=1 -- trivial bound, Iter0
+                    objectives and W after 5 PH iterations on every 64th scenario, x̄ and
+                    conv of each of the 5 iterations, E[obj] after 5
+  farmer1024_cm10   config 2: scen0..scen1023, cm=10 -- trivial bound, sampled Iter0 objectives
+  farmer2048_cm64   the HBM-scale variant of config 3 at test size: scen3..scen2050,
+                    cm=64, 5 PH iterations (scen0..2 skipped: with cm > 1 their crop copies
+                    tie, so their Iter0 LP optimum is a face and only the objective is
+                    solver-independent)
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle.farmer_vec import FarmerVecPH  # noqa: E402
+
+
+def run(names, cm, iters, stride, num_scens=None):
+    t0 = time.time()
+    ph = FarmerVecPH(names, cm, rho=1.0, num_scens=num_scens)
+    tb = ph.iter0()
+    sample = list(range(0, len(names), stride))
+    out = {"names_first": names[0], "names_last": names[-1], "S": len(names), "crops_multiplier": cm,
+           "rho": 1.0, "trivial_bound": tb, "sample": sample,
+           "iter0_obj": ph.iter0_obj[sample].tolist(), "iter0_x": ph.iter0_x[sample].tolist()}
+    if iters:
+        ph.iterk_loop(iters)
+        out["ph_iters"] = iters
+        out["conv"] = [h["conv"] for h in ph.history]
+        out["xbar"] = [h["xbar"].tolist() for h in ph.history]
+        out["W"] = ph.W[sample].tolist()
+        out["x"] = ph.x[sample].tolist()
+        out["Eobj"] = ph.Eobjective()
+    print(f"{len(names)} scen cm={cm}: tb {tb:.10f}  ({time.time() - t0:.1f}s)", flush=True)
+    return out
+
+
+def main():
+    out = {}
+    out["farmer65536_cm1"] = run([f"scen{i}" for i in range(65536)], 1, 5, 64)
+    out["farmer1024_cm10"] = run([f"scen{i}" for i in range(1024)], 10, 0, 8)
+    out["farmer2048_cm64"] = run([f"scen{i}" for i in range(3, 2051)], 64, 5, 16)
+    with open(os.path.join(HERE, "farmer_scale.json"), "w") as f:
+        json.dump(out, f)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""Pin the vectorised farmer oracle (oracle/farmer_vec.py) and the configuration-scale
+fixtures it produced (tests/golden/farmer_scale.json, make_golden_scale.py).
+
+  * Iter0 LP objectives and x against scipy's HiGHS on the explicit row model
+    (oracle.models.farmer_scenario, a restatement of farmer.py:85-224 with no presolve);
+  * PH subproblems against lpqp.farmer_prox_exact, the closed form that reproduces the
+    reference's w_test_data fixtures (test_oracle_golden.py);
+  * the committed fixtures against a fresh recomputation on their sampled scenarios.
+"""
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import farmer_vec as fv
+from oracle.lpqp import solve_lp_highs, farmer_prox_exact
+from oracle.models import farmer_scenario, farmer_yields
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCALE = json.load(open(os.path.join(HERE, "golden", "farmer_scale.json")))
+
+
+@pytest.mark.parametrize("cm,names", [(1, [f"scen{i}" for i in list(range(0, 40)) + [65535, 40001]]),
+                                      (10, [f"scen{i}" for i in range(0, 12)] + ["scen1023"]),
+                                      (64, [f"scen{i}" for i in (3, 4, 5, 700, 2050)])])
+def test_vec_lp_matches_highs(cm, names):
+    warnings.simplefilter("ignore")
+    bp, sl, f0 = fv.pieces(fv.yields(names, cm), cm)
+    x, obj = fv.iter0_lp(bp, sl, f0, 500.0 * cm)
+    for s, nm in enumerate(names):
+        sc = farmer_scenario(nm, cm, num_scens=len(names))
+        A, rl, ru, lb, ub, c, q = sc.arrays()
+        xr, ob, st = solve_lp_highs(A, rl, ru, lb, ub, c)
+        assert st == 0
+        assert abs(ob - obj[s]) <= 1e-12 * abs(ob), (nm, ob, obj[s])
+        if cm == 1 or extract_group(nm) > 0:   # scen0..2 at cm > 1: tied crop copies
+            assert np.abs(xr[sc.nonant_indices()] - x[s]).max() <= 1e-8 * 500 * cm
+
+
+def extract_group(nm):
+    return int(nm[4:]) // 3
+
+
+@pytest.mark.parametrize("cm", [1, 10])
+def test_vec_prox_matches_exact(cm):
+    names = [f"scen{i}" for i in range(3, 23)]
+    bp, sl, f0 = fv.pieces(fv.yields(names, cm), cm)
+    rng = np.random.default_rng(cm)
+    K = 3 * cm
+    W = rng.normal(0, 40, (len(names), K))
+    xbar = np.broadcast_to(500.0 * cm / K * rng.uniform(0.3, 1.7, K), W.shape)
+    rho = rng.uniform(0.5, 2.0, (len(names), K))
+    xv, ov = fv.prox(bp, sl, f0, W, xbar, rho, 500.0 * cm)
+    cs = fv.crops_sorted(cm)
+    for s, nm in enumerate(names):
+        _, Y = farmer_yields(nm, cm)
+        xe, oe = farmer_prox_exact(cs, Y, W[s], xbar[s], rho[s], cm)
+        assert np.abs(xe - xv[s]).max() <= 1e-9, nm
+        assert abs(oe - ov[s]) <= 1e-10 * abs(oe), nm
+
+
+def test_fixture_iter0_samples_recompute():
+    """Fixture Iter0 values are what the oracle gives for those scenarios (spot check)."""
+    for key, names_of in (("farmer65536_cm1", lambda i: f"scen{i}"),
+                          ("farmer1024_cm10", lambda i: f"scen{i}"),
+                          ("farmer2048_cm64", lambda i: f"scen{i + 3}")):
+        g = SCALE[key]
+        cm = g["crops_multiplier"]
+        idx = g["sample"][::max(1, len(g["sample"]) // 8)]
+        names = [names_of(i) for i in idx]
+        bp, sl, f0 = fv.pieces(fv.yields(names, cm), cm)
+        x, obj = fv.iter0_lp(bp, sl, f0, 500.0 * cm)
+        want = np.array(g["iter0_obj"])[[g["sample"].index(i) for i in idx]]
+        assert np.allclose(obj, want, rtol=1e-14, atol=0.0), key
+
+
+def test_fixture_headline_bound_is_the_30_scenario_model():
+    """The config-3 trivial bound sits where the pinned small-case bounds put it: the
+    same model and solver reproduce test_aph.py's -137846 on Scenario1..30."""
+    names = [f"Scenario{i + 1}" for i in range(30)]
+    ph = fv.FarmerVecPH(names, 1)
+    assert round(ph.iter0()) == -137846
+    g = SCALE["farmer65536_cm1"]
+    assert g["S"] == 65536 and len(g["xbar"]) == 5 and len(g["W"]) == len(g["sample"]) == 1024
+    assert -140000 < g["trivial_bound"] < -137000

@@ -49,20 +49,24 @@ def test_oracle_aircond_evaluate_pinned():
 
 
 # ---------------------------------------------------------------- GPU
-def _xe(creator, names, kw, an=None):
+def _xe(creator, names, kw, an=None, solver_options=None):
     from mpisppy_amd.utils.xhat_eval import Xhat_Eval
-    opts = {"iter0_solver_options": None, "iterk_solver_options": None, "display_timing": False,
-            "solver_name": "mi355x_pdhg", "verbose": False, "solver_options": None, "toc": False,
+    opts = {"iter0_solver_options": None, "iterk_solver_options": solver_options, "display_timing": False,
+            "solver_name": "mi355x_pdhg", "verbose": False, "solver_options": solver_options, "toc": False,
             "device": "cuda:0"}
     return Xhat_Eval(opts, names, creator, scenario_denouement=None, all_nodenames=an,
                      scenario_creator_kwargs=kw)
 
 
 @pytest.mark.gpu
-def test_xhat_eval_farmer(gpu):
+@pytest.mark.parametrize("so", [None, {"kernel": 1}, {"gamma": 0.5}, {"kernel": 2}])
+def test_xhat_eval_farmer(gpu, so):
+    """Fixed nonants on every solve kernel: the register kernel (default / 2), the
+    global-memory kernel (1) and another Halpern gamma (which runs on kernel 1); the
+    global-memory kernel's KKT test must use the fixed working bounds."""
     from mpisppy_amd.examples import farmer
     names = farmer.scenario_names_creator(100)
-    ev = _xe(farmer.scenario_creator, names, {"crops_multiplier": 1, "num_scens": 10})
+    ev = _xe(farmer.scenario_creator, names, {"crops_multiplier": 1, "num_scens": 10}, solver_options=so)
     scens = _farmer_scens()
     E = ev.evaluate(FARMER_XHAT)
     oE = xhat_objective(scens, FARMER_XHAT)
@@ -72,6 +76,10 @@ def test_xhat_eval_farmer(gpu):
     oo1 = xhat_objective(scens[:1], FARMER_XHAT) / scens[0].prob
     assert abs(o1 - oo1) <= REL * abs(oo1), (o1, oo1)
     assert round_pos_sig(o1, 2) == -48000.0
+    # calculate_incumbent fixes at the last solve's values: same point, same E
+    assert (ev.engine.host("status") == 0).all()
+    inc = ev.calculate_incumbent()
+    assert inc is not None and abs(inc - E) <= REL * abs(E)
 
 
 @pytest.mark.gpu
