@@ -196,12 +196,15 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
     correction of MI355X_MICROARCH.md) of the same kernel, not from the per-iteration
     byte model, which would exceed the 8 TB/s peak for an on-chip iterate."""
     n, m, nnz, nn = b.n, b.m, b.nnz, b.nn
-    if kinfo["instance"] >= 0:
+    path = kinfo["path"]
+    if path == 2:
         kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}>"
-    elif kinfo.get("wg", 0) > 0:
-        kname = "k_solve_wg"
+        lanes = kinfo["lanes"]
+    elif path == 3:
+        kname = f"k_solve_wg<{kinfo['wKC']}, {kinfo['wZC']}, {kinfo['wKR']}, {kinfo['wZR']}, {kinfo['wps']}>"
+        lanes = 64 * kinfo["wps"]
     else:
-        kname = "k_solve"
+        kname, lanes = "k_solve", 1
     launch_ms = float(np.mean([t for t, _ in launches]))
     units = float(np.mean([u for _, u in launches]))
     F = 4 * nnz + 10 * n + 6 * m
@@ -225,7 +228,7 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
                    "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
                    "note": "measured PMC bytes per launch (profiles/) / HIP-event launch time"},
            "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
-           "kernel": kname, "lanes_per_scenario": kinfo["lanes"], "launch_ms": launch_ms,
+           "kernel": kname, "lanes_per_scenario": lanes, "launch_ms": launch_ms,
            "scenario_iters_per_launch": units, "flops_per_scenario_iter": F,
            "model_bytes_per_scenario_iter": B,
            "model_GBs_if_streamed": B * units / (launch_ms * 1e-3) / 1e9,

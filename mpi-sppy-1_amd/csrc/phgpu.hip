@@ -73,6 +73,10 @@ struct phgpu_state {
     int reg_inst;
     int reg_L, reg_kc, reg_zc, reg_kr, reg_zr;
     int32_t *pl_col_k, *pl_col_r, *pl_row_k, *pl_row_c;
+    // workgroup-per-scenario path (solve_wg.inc): -1 instance = unavailable
+    int wg_inst, wg_long;
+    int32_t *wg_col_id, *wg_row_id, *wg_col_long, *wg_row_long, *wg_col_k, *wg_col_r, *wg_row_k, *wg_row_c;
+    int default_kernel;  // 1 global, 2 register (L <= 64), 3 workgroup per scenario
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
     // PH state (caller-owned)
@@ -527,6 +531,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 }
 
 #include "solve_reg.inc"
+#include "solve_wg.inc"
 
 // ------------------------------------------------------------------ PH reductions
 // phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
@@ -843,6 +848,100 @@ static bool build_plan(int L, int n, int m, const int32_t* row_ptr, const int32_
     return true;
 }
 
+// per-lane VALU estimate of one PDHG iteration of a slot layout, shared by the path
+// choice: a column slot ~ 10 + 2 ZC instructions, a row slot ~ 8 + 2 ZR, each long slot's
+// wave reduction ~ 20.  A scenario costs (lanes / 64) times that.
+static inline long slot_cost(int KC, int ZC, int KR, int ZR, int nlong) {
+    return (long)KC * (10 + 2 * ZC) + (long)KR * (8 + 2 * ZR) + 20L * nlong;
+}
+
+static bool wg_spills(const wg_instance& g) {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, (const void*)g.fn) != hipSuccess) return false;
+    return a.localSizeBytes > REG_SPILL_MAX;
+}
+
+struct wg_plan_host {
+    int nlong = 0, long_per_wave = 0;
+    std::vector<int32_t> col_id, row_id, col_long, row_long, col_k, col_r, row_k, row_c;
+};
+
+// Assign K slots x L lanes to N items (rows or columns) with entry lists ``items``
+// (pairs CSR position, partner index), padded to Z entries per slot.  An item with more
+// than Z entries is long: it takes a whole wave slot (from the last slot / wave
+// backwards), its entries split evenly over the wave's 64 lanes; the short items fill the
+// remaining (slot, lane) positions in order.  False if they do not fit.
+static bool wg_assign(int K, int Z, int W, const std::vector<std::vector<std::pair<int, int>>>& items,
+                      std::vector<int32_t>& id, std::vector<int32_t>& lng, std::vector<int32_t>& ek,
+                      std::vector<int32_t>& eo, int& nlong, std::vector<int>& per_wave) {
+    const int L = WAVE * W;
+    const int N = (int)items.size();
+    id.assign((size_t)K * L, -1);
+    lng.assign((size_t)K * W, 0);
+    ek.assign((size_t)K * L * Z, -1);
+    eo.assign((size_t)K * L * Z, 0);
+    std::vector<char> taken((size_t)K * W, 0);
+    int ws = K * W - 1;
+    for (int a = 0; a < N; ++a) {
+        const int d = (int)items[a].size();
+        if (d <= Z) continue;
+        if (d > WAVE * Z || ws < 0) return false;
+        const int q = ws / W, w = ws % W;
+        --ws;
+        taken[(size_t)q * W + w] = 1;
+        lng[(size_t)q * W + w] = 1;
+        ++nlong;
+        ++per_wave[w];
+        const int per = (d + WAVE - 1) / WAVE;
+        for (int l = 0; l < WAVE; ++l) {
+            const size_t slot = (size_t)q * L + w * WAVE + l;
+            id[slot] = a;
+            for (int z = 0; z < per; ++z) {
+                const int e = l * per + z;
+                if (e >= d) break;
+                ek[slot * Z + z] = items[a][e].first;
+                eo[slot * Z + z] = items[a][e].second;
+            }
+        }
+    }
+    long pos = 0;  // q-major over (slot, lane)
+    for (int a = 0; a < N; ++a) {
+        const int d = (int)items[a].size();
+        if (d > Z) continue;
+        while (pos < (long)K * L && taken[(size_t)(pos / L) * W + (pos % L) / WAVE])
+            pos = (pos / WAVE + 1) * WAVE;     // skip the rest of a long-item wave slot
+        if (pos >= (long)K * L) return false;
+        const size_t slot = (size_t)pos;
+        id[slot] = a;
+        for (int z = 0; z < d; ++z) {
+            ek[slot * Z + z] = items[a][z].first;
+            eo[slot * Z + z] = items[a][z].second;
+        }
+        ++pos;
+    }
+    return true;
+}
+
+// Plan of solve_wg.inc for one instance.
+static bool build_wg_plan(const wg_instance& g, int n, int m, const int32_t* row_ptr, const int32_t* col_idx,
+                          wg_plan_host& out) {
+    if (m < 1 || n < 1) return false;
+    std::vector<std::vector<std::pair<int, int>>> cols(n), rows(m);
+    for (int i = 0; i < m; ++i)
+        for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+            cols[col_idx[k]].push_back({k, i});
+            rows[i].push_back({k, col_idx[k]});
+        }
+    std::vector<int> pwc(g.WPS, 0), pwr(g.WPS, 0);
+    int nl = 0;
+    if (!wg_assign(g.KC, g.ZC, g.WPS, cols, out.col_id, out.col_long, out.col_k, out.col_r, nl, pwc)) return false;
+    if (!wg_assign(g.KR, g.ZR, g.WPS, rows, out.row_id, out.row_long, out.row_k, out.row_c, nl, pwr)) return false;
+    out.nlong = nl;
+    out.long_per_wave = 0;
+    for (int w = 0; w < g.WPS; ++w) out.long_per_wave = std::max(out.long_per_wave, pwc[w] + pwr[w]);
+    return true;
+}
+
 // ------------------------------------------------------------------ C-ABI
 template <typename T>
 static int dalloc(phgpu_state* h, T** p, size_t count) {
@@ -1077,6 +1176,64 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
             h->reg_zr = zr;
         }
     }
+    // workgroup-per-scenario path: the cheapest non-spilling instance by slot_cost x waves
+    // per scenario (PHGPU_WPS=<waves> pins the waves per scenario)
+    h->wg_inst = -1;
+    {
+        const char* env = getenv("PHGPU_WPS");
+        const int pinned = env ? atoi(env) : 0;
+        const int ninst = (int)(sizeof(g_wg_instances) / sizeof(g_wg_instances[0]));
+        long best = 0;
+        wg_plan_host bp;
+        for (int a = 0; a < ninst; ++a) {
+            const wg_instance& g = g_wg_instances[a];
+            if (pinned > 0 && g.WPS != pinned) continue;
+            wg_plan_host p;
+            if (!build_wg_plan(g, n, m, row_ptr, col_idx, p)) continue;
+            if (wg_spills(g)) continue;
+            const long cost = (long)g.WPS * slot_cost(g.KC, g.ZC, g.KR, g.ZR, p.long_per_wave);
+            if (h->wg_inst < 0 || cost < best) {
+                h->wg_inst = a;
+                best = cost;
+                bp = std::move(p);
+            }
+        }
+        if (h->wg_inst >= 0) {
+            int rc2 = 0;
+            rc2 |= dalloc(h, &h->wg_col_id, bp.col_id.size());
+            rc2 |= dalloc(h, &h->wg_row_id, bp.row_id.size());
+            rc2 |= dalloc(h, &h->wg_col_long, bp.col_long.size());
+            rc2 |= dalloc(h, &h->wg_row_long, bp.row_long.size());
+            rc2 |= dalloc(h, &h->wg_col_k, bp.col_k.size());
+            rc2 |= dalloc(h, &h->wg_col_r, bp.col_r.size());
+            rc2 |= dalloc(h, &h->wg_row_k, bp.row_k.size());
+            rc2 |= dalloc(h, &h->wg_row_c, bp.row_c.size());
+            if (rc2) {
+                phgpu_destroy(h);
+                return set_err(-3, "workgroup plan allocation failed");
+            }
+            struct { int32_t* d; std::vector<int32_t>* v; } up[] = {
+                {h->wg_col_id, &bp.col_id}, {h->wg_row_id, &bp.row_id}, {h->wg_col_long, &bp.col_long},
+                {h->wg_row_long, &bp.row_long}, {h->wg_col_k, &bp.col_k}, {h->wg_col_r, &bp.col_r},
+                {h->wg_row_k, &bp.row_k}, {h->wg_row_c, &bp.row_c}};
+            for (auto& u : up)
+                if (e == hipSuccess) e = hipMemcpy(u.d, u.v->data(), u.v->size() * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                phgpu_destroy(h);
+                return set_err(-2, "workgroup plan upload failed: %s", hipGetErrorString(e));
+            }
+            h->wg_long = bp.nlong;
+        }
+        // default path: the cheaper per scenario (register path at its chosen L)
+        long reg_cost_s = -1;
+        if (h->reg_inst >= 0) {
+            const reg_instance& r = g_reg_instances[h->reg_inst];
+            reg_cost_s = (long)h->reg_L * slot_cost(r.KC, r.ZC, r.KR, r.ZR, 0) / WAVE;
+        }
+        if (h->reg_inst >= 0 && (h->wg_inst < 0 || reg_cost_s <= best)) h->default_kernel = 2;
+        else if (h->wg_inst >= 0) h->default_kernel = 3;
+        else h->default_kernel = 1;
+    }
     *out = h;
     return 0;
 }
@@ -1162,14 +1319,43 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
     P.wmin = 1.0 / P.wmax;
     hipStream_t st = (hipStream_t)stream;
-    // the register-resident kernel is specialised for the reflected step (gamma = 1, the
+    // the register-resident kernels are specialised for the reflected step (gamma = 1, the
     // default); another gamma runs on the global-memory kernel
-    const bool use_reg = (o.kernel == 2) || (o.kernel == 0 && h->reg_inst >= 0 && o.gamma == 1.0);
+    if (o.kernel < 0 || o.kernel > 3) return set_err(-1, "bad kernel option %d", o.kernel);
     if (o.kernel == 2 && h->reg_inst < 0)
         return set_err(-1, "register-resident kernel requested but no compiled instance fits this pattern");
-    if (o.kernel == 2 && o.gamma != 1.0)
-        return set_err(-1, "register-resident kernel requires gamma = 1 (got %g)", o.gamma);
-    if (use_reg) {
+    if (o.kernel == 3 && h->wg_inst < 0)
+        return set_err(-1, "workgroup-per-scenario kernel requested but no compiled instance fits this pattern");
+    if ((o.kernel == 2 || o.kernel == 3) && o.gamma != 1.0)
+        return set_err(-1, "register-resident kernels require gamma = 1 (got %g)", o.gamma);
+    const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? h->default_kernel : 1);
+    const bool use_reg = path == 2;
+    if (path == 3) {
+        const wg_instance& gi = g_wg_instances[h->wg_inst];
+        wg_plan pl;
+        pl.L = WAVE * gi.WPS;
+        pl.kc = gi.KC;
+        pl.zc = gi.ZC;
+        pl.kr = gi.KR;
+        pl.zr = gi.ZR;
+        pl.col_id = h->wg_col_id;
+        pl.row_id = h->wg_row_id;
+        pl.col_long = h->wg_col_long;
+        pl.row_long = h->wg_row_long;
+        pl.col_k = h->wg_col_k;
+        pl.col_r = h->wg_col_r;
+        pl.row_k = h->wg_row_k;
+        pl.row_c = h->wg_row_c;
+        const size_t lds = wg_lds_doubles(h->n, h->m, gi.KC, gi.KR, gi.WPS) * sizeof(double);
+        int per_cu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gi.fn, pl.L, lds));
+        if (per_cu < 1) per_cu = 1;
+        int64_t nblk = (int64_t)per_cu * h->num_cus;
+        if (nblk > h->S) nblk = h->S;
+        HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
+        hipLaunchKernelGGL(gi.fn, dim3((unsigned)nblk), dim3(pl.L), lds, st, *h, P, pl, h->qhead, x, y, obj, bound,
+                           status, iters);
+    } else if (use_reg) {
         reg_plan pl;
         pl.L = h->reg_L;
         pl.kc = h->reg_kc;
@@ -1262,7 +1448,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->node_of, h->Ah_csr, h->Ah_csc, h->Dr, h->Dc, h->normA, h->lbh, h->ubh,
                     h->rlh, h->ruh, h->ch, h->qh, h->x, h->x0, h->xe, h->xt, h->aty, h->aty0,
                     h->y, h->y0, h->yt, h->omega, h->part, h->part_node, h->pl_col_k,
-                    h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead};
+                    h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead, h->wg_col_id, h->wg_row_id,
+                    h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -1280,8 +1467,11 @@ extern "C" int64_t phgpu_workspace_bytes(phgpu_handle h) { return h ? h->ws_byte
 
 extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     if (!h || !info) return set_err(-1, "null argument");
+    // info[0..9]: the register path (L <= 64); info[10..15]: the workgroup path; info[16]:
+    // the path phgpu_solve takes by default (1 global, 2 register, 3 workgroup)
+    for (int k = 0; k < 17; ++k) info[k] = 0;
     info[0] = h->reg_inst;
-    info[1] = h->reg_L;
+    info[1] = h->reg_inst >= 0 ? h->reg_L : 0;
     info[2] = h->reg_kc;
     info[3] = h->reg_zc;
     info[4] = h->reg_kr;
@@ -1292,8 +1482,16 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
         info[7] = r.ZC;
         info[8] = r.KR;
         info[9] = r.ZR;
-    } else {
-        info[6] = info[7] = info[8] = info[9] = 0;
     }
+    info[10] = h->wg_inst;
+    if (h->wg_inst >= 0) {
+        const wg_instance& g = g_wg_instances[h->wg_inst];
+        info[11] = g.WPS;
+        info[12] = g.KC;
+        info[13] = g.ZC;
+        info[14] = g.KR;
+        info[15] = g.ZR;
+    }
+    info[16] = h->default_kernel;
     return 0;
 }

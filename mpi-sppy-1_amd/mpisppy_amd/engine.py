@@ -133,9 +133,10 @@ class PHEngine:
 
     def kernel_info(self):
         """Which solve kernel the handle uses (phgpu_kernel_info)."""
-        info = (ctypes.c_int32 * 10)()
+        info = (ctypes.c_int32 * 17)()
         _lib.check(self.lib.phgpu_kernel_info(self.h, info), "phgpu_kernel_info")
-        keys = ["instance", "lanes", "kc", "zc", "kr", "zr", "KC", "ZC", "KR", "ZR"]
+        keys = ["instance", "lanes", "kc", "zc", "kr", "zr", "KC", "ZC", "KR", "ZR",
+                "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state

@@ -86,7 +86,7 @@ def test_headline_instance_on_a_slice(gpu):
     os.environ["PHGPU_LANES"] = "4"
     try:
         names = [f"scen{i}" for i in range(0, 65536, 16)]
-        ph = _farmer_ph(names, 1, 65536)
+        ph = _farmer_ph(names, 1, len(names))
         ph._create_solvers()
         info = ph.engine.kernel_info()
     finally:

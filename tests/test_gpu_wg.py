@@ -1,0 +1,152 @@
+"""The workgroup-per-scenario solve kernel (k_solve_wg, solve_wg.inc): long rows and
+long columns spread over a wave, multi-wave scenarios, and the farmer cm = 64 variant of
+config 3 against the committed oracle fixtures (tests/golden/farmer_scale.json)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCALE = json.load(open(os.path.join(HERE, "golden", "farmer_scale.json")))
+OBJ_REL = 1e-5
+ABS = 1e-5
+
+
+def _long_row_col_batch(S, seed, n=70, m=40, with_q=False):
+    """Random feasible LPs sharing one pattern: a sparse part with 3 entries per row and
+    at most 2 per column, plus one dense row over every column (a long row: 70 > ZR)
+    and one dense column 0 in every row (a long column: 41 > ZC)."""
+    from mpisppy_amd.batch import ScenarioBatch
+    rng = np.random.default_rng(seed)
+    cap = np.full(n, 2)
+    cap[0] = 0
+    rows = []
+    for i in range(m):
+        avail = np.nonzero(cap > 0)[0]
+        cols = sorted(rng.choice(avail, size=3, replace=False).tolist())
+        cap[cols] -= 1
+        rows.append([0] + cols)
+    rows.append(list(range(n)))
+    row_ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    col_idx = np.array([j for r in rows for j in r], dtype=np.int32)
+    M = len(rows)
+    nnz = col_idx.size
+    A = rng.normal(size=(S, nnz))
+    x_feas = rng.uniform(0.0, 5.0, size=(S, n))
+    Ax = np.zeros((S, M))
+    r_of = np.repeat(np.arange(M), np.diff(row_ptr))
+    for k in range(nnz):
+        Ax[:, r_of[k]] += A[:, k] * x_feas[:, col_idx[k]]
+    kind = rng.integers(0, 3, size=M)
+    rl = np.where(kind == 1, -np.inf, Ax - rng.uniform(0.1, 2.0, size=(S, M)))
+    ru = np.where(kind == 0, np.inf, Ax + rng.uniform(0.1, 2.0, size=(S, M)))
+    eq = kind == 2
+    rl[:, eq] = Ax[:, eq]
+    ru[:, eq] = Ax[:, eq]
+    lb = np.zeros((S, n))
+    ub = np.full((S, n), 10.0)
+    c = rng.normal(size=(S, n))
+    q = rng.uniform(0.0, 1.0, size=(S, n)) if with_q else np.zeros((S, n))
+    nn = 2
+    return ScenarioBatch([f"s{i}" for i in range(S)], row_ptr, col_idx, A, c, lb, ub, rl, ru, q,
+                         np.zeros(S), np.arange(nn, dtype=np.int32), np.zeros(nn, np.int32),
+                         np.arange(nn, dtype=np.int32), np.zeros((S, 1), np.int32), ["ROOT"],
+                         np.full(S, 1.0 / S), np.full((S, 1), 1.0 / S))
+
+
+@pytest.mark.parametrize("S,with_q,wps", [(5, False, "1"), (67, True, "1"), (40, False, "4")])
+def test_long_row_and_column_vs_highs(gpu, S, with_q, wps):
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    from oracle.lpqp import solve_lp_highs, solve_qp_ipm
+    b = _long_row_col_batch(S, seed=S, with_q=with_q)
+    os.environ["PHGPU_WPS"] = wps
+    try:
+        e = PHEngine(b, device="cuda:0")
+    finally:
+        del os.environ["PHGPU_WPS"]
+    info = e.kernel_info()
+    assert info["wg_instance"] >= 0 and info["wps"] == int(wps), info
+    e.solve(_lib.default_options(kernel=3), warm=False)
+    st, obj, bnd, x = e.host("status"), e.host("obj"), e.host("bound"), e.host("x")
+    assert (st == _lib.OPTIMAL).all(), st
+    for s in range(S):
+        A = b.dense_A(s)
+        if with_q:
+            xr, ob, rc = solve_qp_ipm(A, b.rl[s], b.ru[s], b.lb[s], b.ub[s], b.c[s], b.q[s])
+        else:
+            xr, ob, rc = solve_lp_highs(A, b.rl[s], b.ru[s], b.lb[s], b.ub[s], b.c[s])
+        assert rc == 0
+        tol = OBJ_REL * max(1.0, abs(ob))
+        assert abs(obj[s] - ob) <= tol and abs(bnd[s] - ob) <= tol, (s, obj[s], bnd[s], ob)
+        ax = A @ x[s]
+        assert np.all(ax >= b.rl[s] - 1e-6 * (1 + np.abs(b.rl[s])))
+        assert np.all(ax <= b.ru[s] + 1e-6 * (1 + np.abs(b.ru[s])))
+    # the global-memory kernel agrees; a warm start reproduces the answer
+    o3 = obj.copy()
+    e.solve(_lib.default_options(kernel=1), warm=False)
+    assert np.all(np.abs(e.host("obj") - o3) <= OBJ_REL * np.maximum(1.0, np.abs(o3)))
+    e.solve(_lib.default_options(kernel=3), warm=True)
+    assert np.all(np.abs(e.host("obj") - o3) <= OBJ_REL * np.maximum(1.0, np.abs(o3)))
+    e.close()
+
+
+@pytest.mark.parametrize("kind,code", [("primal", 2), ("dual", 3)])
+def test_wg_kernel_certifies_infeasibility(gpu, kind, code):
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    b = _long_row_col_batch(6, seed=3)
+    bad = 4
+    if kind == "primal":          # the long row above what the bounds allow
+        b.rl[bad, -1] = 1e6
+        b.ru[bad, -1] = np.inf
+    else:                         # a free column with negative cost in no bounded direction
+        b.ub[bad, 5] = np.inf
+        b.lb[bad, 5] = -np.inf
+        b.c[bad, 5] = -1.0
+        b.rl[bad, :] = -np.inf
+        b.ru[bad, :] = np.inf
+    e = PHEngine(b, device="cuda:0")
+    e.solve(_lib.default_options(kernel=3), warm=False)
+    st = e.host("status")
+    assert st[bad] == code, (st, e.host("iters"))
+    assert (np.delete(st, bad) == 0).all()
+    e.close()
+
+
+def test_farmer_cm64_parity(gpu):
+    """The HBM-scale variant of config 3 (cm = 64: n = 768, m = 385, a 192-entry acreage
+    row) at test size: scen3..scen2050, 5 PH iterations vs the exact oracle."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    g = SCALE["farmer2048_cm64"]
+    names = [f"scen{i}" for i in range(3, 2051)]
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": -1.0,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": farmer.batch_creator}
+    ph = PH(opts, names, farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": 64, "num_scens": len(names)})
+    ph.PH_Prep()
+    info = ph.engine.kernel_info()
+    assert info["path"] == 3 and info["wps"] >= 2, info
+    tb = ph.Iter0()
+    assert (ph.engine.host("status") == 0).all()
+    assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"]), (tb, g["trivial_bound"])
+    smp = np.array(g["sample"])
+    obj0 = ph.engine.host("obj")[smp]
+    assert np.all(np.abs(obj0 - g["iter0_obj"]) <= OBJ_REL * np.abs(g["iter0_obj"]))
+    for it in range(5):
+        ph.Compute_Xbar()
+        ph.Update_W()
+        conv = ph.convergence_diff()
+        xb = ph.xbar_by_node()["ROOT"][:192]
+        assert np.abs(xb - np.array(g["xbar"][it])).max() <= ABS, (it, np.abs(xb - g["xbar"][it]).max())
+        assert abs(conv - g["conv"][it]) <= ABS, (it, conv, g["conv"][it])
+        ph.solve_loop(solver_options=ph.iterk_solver_options, gripe=True)
+        assert (ph.engine.host("status") == 0).all()
+    err = np.abs(ph.W_array()[smp] - np.array(g["W"]))
+    assert err.max() <= ABS, (err.max(), int(smp[err.max(1).argmax()]))
+    assert abs(ph.Eobjective() - g["Eobj"]) <= OBJ_REL * abs(g["Eobj"])
