@@ -130,6 +130,29 @@ def iter0_lp(bp, sl, f0, total):
     return x, obj
 
 
+def lp_margin(bp, sl, total):
+    """Conditioning of the Iter0 LP: the slope gap between the marginal segment (the one
+    the acreage row cuts) and its nearest neighbour in slope order ([S]; inf when the
+    acreage row is slack).  A tiny margin is a near-tie: the optimum is unique but a
+    first-order method needs ~1/margin iterations to pick the right crop."""
+    S, K, J = sl.shape
+    length = np.diff(bp, axis=-1).reshape(S, K * J)
+    slope = sl.reshape(S, K * J)
+    order = np.argsort(slope, axis=1, kind="stable")
+    s_o = np.take_along_axis(slope, order, 1)
+    l_o = np.where(s_o < 0.0, np.take_along_axis(length, order, 1), 0.0)
+    cum = np.cumsum(l_o, axis=1)
+    out = np.full(S, np.inf)
+    for s in range(S):
+        k = int(np.searchsorted(cum[s], total))
+        if k >= K * J or s_o[s, k] >= 0.0:
+            continue
+        nb = [abs(s_o[s, k] - s_o[s, kk]) for kk in (k - 1, k + 1)
+              if 0 <= kk < K * J and l_o[s, kk] > 0 and kk != k]
+        out[s] = min(nb) if nb else np.inf
+    return out
+
+
 def _x_of_lam(bp, sl, lin, rho, xbar, lam):
     a = xbar[..., None] - (sl + (lin + lam[:, None])[..., None]) / rho[..., None]
     return bp[..., 0] + np.clip(a - bp[..., :-1], 0.0, np.diff(bp, axis=-1)).sum(-1)

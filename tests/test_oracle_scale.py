@@ -65,7 +65,7 @@ def test_fixture_iter0_samples_recompute():
     """Fixture Iter0 values are what the oracle gives for those scenarios (spot check)."""
     for key, names_of in (("farmer65536_cm1", lambda i: f"scen{i}"),
                           ("farmer1024_cm10", lambda i: f"scen{i}"),
-                          ("farmer2048_cm64", lambda i: f"scen{i + 3}")):
+                          ("farmer2048_cm64", lambda i: SCALE["farmer2048_cm64"]["names"][i])):
         g = SCALE[key]
         cm = g["crops_multiplier"]
         idx = g["sample"][::max(1, len(g["sample"]) // 8)]
@@ -85,3 +85,11 @@ def test_fixture_headline_bound_is_the_30_scenario_model():
     g = SCALE["farmer65536_cm1"]
     assert g["S"] == 65536 and len(g["xbar"]) == 5 and len(g["W"]) == len(g["sample"]) == 1024
     assert -140000 < g["trivial_bound"] < -137000
+
+
+def test_cm64_fixture_set_is_well_conditioned():
+    g = SCALE["farmer2048_cm64"]
+    bp, sl, _ = fv.pieces(fv.yields(g["names"], 64), 64)
+    assert fv.lp_margin(bp, sl, 32000.0).min() >= 1e-2
+    t = SCALE["farmer_cm64_neartie"]
+    assert "scen411" in t["names"] and max(t["margin"]) < 1e-3

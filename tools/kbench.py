@@ -14,7 +14,7 @@ names = farmer.scenario_names_creator(S)
 b = farmer.batch_creator(names, crops_multiplier=cm, num_scens=S)
 ref = None
 for L in lanes:
-    for kern in ([1, 2] if (L == lanes[0] and not extra) else [2]):
+    for kern in ([1, 0] if (L == lanes[0] and not extra and os.environ.get('KB_GLOBAL')) else [0]):
         if L:
             os.environ["PHGPU_LANES"] = str(L)
         else:
@@ -35,7 +35,7 @@ for L in lanes:
         it = e.host("iters"); st = e.host("status")
         W = e.host("W")
         if ref is None: ref = W.copy()
-        print(f"kernel={kern} L={info['lanes']} inst=({info['KC']},{info['ZC']},{info['KR']},{info['ZR']}) "
+        print(f"kernel={kern} path={info['path']} L={info['lanes']} inst=({info['KC']},{info['ZC']},{info['KR']},{info['ZR']}) wg=({info['wKC']},{info['wZC']},{info['wKR']},{info['wZR']},{info['wps']}) "
               f"iter0 {t0:.2f} ms (max it {it0.max()}) | PH solves ms {['%.2f' % t for t in times]} "
               f"max it {it.max()} mean {it.mean():.0f} | us/iter(max) {1e3 * times[-1] / max(1, it.max()):.2f} "
               f"| nonopt {(st != 0).sum()} | W dev vs first {np.abs(W - ref).max():.2e}", flush=True)
