@@ -15,15 +15,21 @@ import torch
 from .. import global_toc
 from .spcommunicator import SPCommunicator
 from .spoke import ConvergerSpokeType
+from . import transport as tp
 
 logger = logging.getLogger("mpisppy_amd.cylinders.hub")
 
 
 class Hub(SPCommunicator):
     def __init__(self, spbase_object, fullcomm=None, strata_comm=None, cylinder_comm=None, spokes=None,
-                 options=None):
+                 options=None, layout=None):
         super().__init__(spbase_object, fullcomm, strata_comm, cylinder_comm, options)
-        self.spokes = list(spokes or [])      # spoke OBJECTS (co-located), not spoke dicts
+        # co-located: spoke OBJECTS driven from sync(); on their own ranks (``layout``, a
+        # transport.CylinderLayout): spoke CLASSES, reached through transport ports
+        self.spokes = list(spokes or [])
+        self.layout = layout
+        self.ports = {}
+        self._remote = {}
         self.n_spokes = len(self.spokes)
         self.latest_ib_char = None
         self.latest_ob_char = None
@@ -44,7 +50,7 @@ class Hub(SPCommunicator):
         self.outerbound_spoke_chars = dict()
         self.innerbound_spoke_chars = dict()
         for i, spoke in enumerate(self.spokes):
-            cls = type(spoke)
+            cls = spoke if isinstance(spoke, type) else type(spoke)
             for cst in getattr(cls, "converger_spoke_types", ()):
                 if cst == ConvergerSpokeType.OUTER_BOUND:
                     self.outerbound_spoke_indices.add(i + 1)
@@ -177,6 +183,12 @@ class Hub(SPCommunicator):
 
     # hub.py:396-436: a bound is new when the spoke's write id advanced
     def hub_from_spoke(self, idx):
+        if self.layout is not None:
+            bound, wid = self._remote.get(idx, (math.nan, 0))
+            if wid > self._spoke_seen.get(idx, 0):
+                self._spoke_seen[idx] = wid
+                return True, bound
+            return False, None
         spoke = self.spokes[idx - 1]
         wid = spoke.local_write_id
         if wid > self._spoke_seen.get(idx, 0):
@@ -207,11 +219,38 @@ class Hub(SPCommunicator):
 
     # hub.py:438-452
     def send_terminate(self):
+        if self.layout is not None:
+            for idx in sorted(self.ports):
+                self._answer(idx, tp.KILL)
+            return
         for spoke in self.spokes:
             spoke._terminate()
 
+    # spokes on their own ranks: answer a spoke's pending Get with the window it reads
+    def _window_values(self, idx):
+        return None
+
+    def _answer(self, idx, write_id):
+        vals = self._window_values(idx)
+        bound, wid = self.ports[idx].answer(None if vals is None else tp.ci_order(vals), self.BestOuterBound,
+                                            self.BestInnerBound, write_id)
+        if wid > self._remote.get(idx, (math.nan, 0))[1]:
+            self._remote[idx] = (bound, wid)
+
+    def serve_spokes(self):
+        """One pass over the spokes' Gets (the reference's hub_to_spoke Puts, hub.py:369-395):
+        answered only when every hub rank has its peer's request (MIN agreement)."""
+        idxs = sorted(self.ports)
+        ok = tp.agree_ready(self.layout, [self.ports[i].ready() for i in idxs])
+        for i, go in zip(idxs, ok):
+            if go:
+                self._answer(i, float(self._hub_write_id))
+
     # hub.py:163-172
     def hub_finalize(self):
+        if self.layout is not None:
+            # the spokes' last bounds arrived with their final Gets (send_terminate)
+            pass
         if self.has_outerbound_spokes:
             self.receive_outerbounds()
         if self.has_innerbound_spokes:
@@ -231,6 +270,11 @@ class PHHub(Hub):
             logger.warning("No InnerBound Spokes defined, this converger will not cause the hub to terminate")
         self._w_snapshot = None
         self._nonant_snapshot = None
+        if self.layout is not None:
+            nn, S = max(self.opt.batch.nn, 1), self.opt.batch.S
+            for idx in sorted(self.w_spoke_indices | self.nonant_spoke_indices | self.bounds_only_indices):
+                self.ports[idx] = tp.HubPort(self.layout, idx, nn * S)
+            return
         # spokes prepare (their own Iter0-equivalent work) before the hub's Iter0
         for spoke in self.spokes:
             spoke.main()
@@ -238,6 +282,13 @@ class PHHub(Hub):
     # hub.py:501-514
     def sync(self):
         self._hub_write_id += 1
+        if self.layout is not None:
+            self.serve_spokes()
+            if self.has_outerbound_spokes:
+                self.receive_outerbounds()
+            if self.has_innerbound_spokes:
+                self.receive_innerbounds()
+            return
         if self.has_w_spokes:
             self.send_ws()
         if self.has_nonant_spokes:
@@ -276,9 +327,19 @@ class PHHub(Hub):
     def main(self):
         self.opt.ph_main(finalize=False)
 
+    def _window_values(self, idx):
+        if idx in self.w_spoke_indices:
+            return self.opt.engine.W[: max(self.opt.batch.nn, 1)]
+        if idx in self.nonant_spoke_indices:
+            return self.opt.engine.nonant_x_dev()
+        return None
+
     def send_terminate(self):
         # the final W (updated at the top of the last PH iteration) goes out with the
         # kill signal so W spokes can do their final pass (lagrangian_bounder.py:82-95)
+        if self.layout is not None:
+            self._hub_write_id += 1
+            return super().send_terminate()
         if self.has_w_spokes:
             self._hub_write_id += 1
             self.send_ws()

@@ -36,6 +36,7 @@ class Spoke(SPCommunicator):
         self._killed = False
         self._new_locals = False
         self._locals = None
+        self._remote = False      # True when the spoke runs on its own ranks (run_remote)
 
     # hub -> spoke (hub.py:370-395 Put; here a reference to the hub's snapshot)
     def _deliver(self, write_id, tensor):
@@ -58,8 +59,38 @@ class Spoke(SPCommunicator):
         return False
 
     def got_kill_signal(self):
+        if self._remote:          # the Get of run_remote already took the window
+            return self._killed
         self._new_locals = self.spoke_from_hub()
         return self._killed
+
+    # spoke.py:186-214 (the spoke's own loop when it has ranks of its own): prepare, then
+    # alternate a Get of the hub's window with one pass of the loop body until the kill
+    # signal; ``port`` is a transport.SpokePort
+    def run_remote(self, port):
+        from . import transport as tp
+        self._remote = True
+        self.main()
+        nn, S = max(self.opt.batch.nn, 1), self.opt.batch.S
+        device = self.opt.engine.device if self.opt.engine is not None else None
+        while True:
+            bound = getattr(self, "_bound", float("nan"))
+            vals, outer, inner, wid = port.get(bound, self.local_write_id, self.remote_write_id)
+            if device is None and self.opt.engine is not None:
+                device = self.opt.engine.device
+            t = tp.from_ci_order(vals, nn, S, device)
+            if self._locals is None or self._locals.shape != t.shape:
+                self._locals = t
+            else:
+                self._locals.copy_(t)
+            self.hub_outer_bound, self.hub_inner_bound = outer, inner
+            self._new_locals = True
+            if wid == tp.KILL:
+                self._killed = True
+                break
+            self.remote_write_id = int(wid)
+            self.do_work()
+        return self.finalize()
 
     def get_serial_number(self):
         return self.remote_write_id

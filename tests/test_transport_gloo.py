@@ -1,0 +1,106 @@
+"""Hub <-> spoke transport on separate ranks (cylinders/transport.py) with gloo on CPU.
+
+A stand-in hub (P ranks) runs 12 "PH iterations"; at each sync it answers its strata
+peer's Get with a window of values that encode (iteration, hub rank), a write id and the
+trailing bound slots (hub.py:281-285).  A stand-in spoke (P ranks) does a Get, checks
+the window, 'works' for a while and returns a bound that encodes what it saw.  Checked:
+write ids advance, every rank of the spoke sees the same hub iteration (the MIN
+agreement over hub ranks), the values are the hub's in 'ci' order, bounds reach the hub
+with their write ids, and the kill signal (-1, hub.py:438-450) ends the spoke's loop.
+"""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+NN, S = 3, 5
+
+
+def _worker(rank, world, port, out_dir, n_spokes):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "mpi-sppy-1_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.cylinders import transport as tp
+        lay = tp.CylinderLayout(1 + n_spokes)
+        log = []
+        if lay.cylinder == 0:
+            ports = {k: tp.HubPort(lay, k, NN * S) for k in range(1, n_spokes + 1)}
+            got = {}
+            for it in range(1, 13):
+                W = torch.arange(NN * S, dtype=torch.float64).reshape(NN, S) + 1000 * it + 100 * lay.cyl_rank
+                ok = tp.agree_ready(lay, [ports[k].ready() for k in sorted(ports)])
+                for k, go in zip(sorted(ports), ok):
+                    if go:
+                        b, wid = ports[k].answer(tp.ci_order(W), -1.0 * it, 2.0 * it, float(it))
+                        got.setdefault(k, []).append((it, b, wid))
+                        log.append((it, k))
+                time.sleep(0.01)
+            for k in sorted(ports):
+                b, wid = ports[k].answer(tp.ci_order(W), 0.0, 0.0, tp.KILL)
+                got.setdefault(k, []).append((13, b, wid))
+            np.save(os.path.join(out_dir, f"hub{rank}.npy"),
+                    np.array([(k, it, b, wid) for k, v in got.items() for (it, b, wid) in v]))
+        else:
+            p = tp.SpokePort(lay, NN * S)
+            bound, bwid, seen = float("nan"), 0, 0
+            rows = []
+            while True:
+                vals, outer, inner, wid = p.get(bound, bwid, seen)
+                if wid == tp.KILL:
+                    rows.append((-1, -1, -1, -1))
+                    break
+                W = tp.from_ci_order(vals, NN, S, "cpu")
+                it = int(wid)
+                assert wid > seen
+                assert torch.equal(W, torch.arange(NN * S, dtype=torch.float64).reshape(NN, S)
+                                   + 1000 * it + 100 * lay.cyl_rank)
+                assert outer == -1.0 * it and inner == 2.0 * it
+                seen = it
+                rows.append((it, lay.cylinder, lay.cyl_rank, 0))
+                time.sleep(0.025 * lay.cylinder)          # spokes work at different speeds
+                bound, bwid = 10.0 * it + lay.cylinder, bwid + 1
+            np.save(os.path.join(out_dir, f"spoke{rank}.npy"), np.array(rows))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world,n_spokes", [(3, 2), (4, 1), (6, 2)])
+def test_transport_windows(tmp_path, world, n_spokes):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_spokes), nprocs=world, join=True)
+    P = world // (1 + n_spokes)
+    hubs = [np.load(tmp_path / f"hub{r}.npy") for r in range(P)]
+    # every hub rank answered each spoke at the same iterations (MIN agreement)
+    for h in hubs[1:]:
+        assert np.array_equal(h[:, :2], hubs[0][:, :2])
+    for k in range(1, n_spokes + 1):
+        ans = hubs[0][hubs[0][:, 0] == k]
+        its = ans[:, 1]
+        assert its[-1] == 13 and np.all(np.diff(its) > 0) and len(its) >= 3
+        # the bound that came back with each Get is the one computed from the previous
+        # answer (10 * iteration + spoke), with an advancing write id
+        for prev, cur in zip(ans[:-1], ans[1:]):
+            assert cur[2] == 10 * prev[1] + k and cur[3] > prev[3]
+        for r in range(P):
+            sp = np.load(tmp_path / f"spoke{k * P + r}.npy")
+            assert sp[-1][0] == -1
+            assert list(sp[:-1, 0]) == list(its[:-1])

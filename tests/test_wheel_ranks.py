@@ -1,0 +1,74 @@
+"""The farmer wheel (PH hub + Lagrangian + xhatshuffle) with every cylinder on its own
+ranks -- the reference's placement (spin_the_wheel.py:219-237) -- and the hub <-> spoke
+windows of cylinders/transport.py.  Ranks are gloo processes sharing cuda:0 (1 or 2 per
+cylinder).  The asynchronous schedule changes the bound trajectory, so the check is on
+what does not depend on it: the outer bound is valid (<= the EF optimum), the inner
+bound reaches the EF optimum (test_sc.py:30-38: x* = 80/250/170, obj -108390), the gap
+closes to rel_gap, and every rank learns the same final bounds."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FARMER_EF_OBJ = -108390.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    from types import SimpleNamespace
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "mpi-sppy-1_amd"))
+    sys.path.insert(0, root)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.examples import farmer
+        from mpisppy_amd.spin_the_wheel import WheelSpinner
+        from mpisppy_amd.utils import cfg_vanilla as vanilla
+        names = farmer.scenario_names_creator(3)
+        cfg = SimpleNamespace(solver_name="mi355x_pdhg", default_rho=1.0, max_iterations=300, rel_gap=1e-4,
+                              intra_hub_conv_thresh=1e-10, device="cuda:0", toc=False)
+        kw = {"num_scens": 3}
+        hub = vanilla.ph_hub(cfg, farmer.scenario_creator, None, names, scenario_creator_kwargs=kw)
+        spokes = [vanilla.lagrangian_spoke(cfg, farmer.scenario_creator, None, names, scenario_creator_kwargs=kw),
+                  vanilla.xhatshuffle_spoke(cfg, farmer.scenario_creator, None, names, scenario_creator_kwargs=kw)]
+        ws = WheelSpinner(hub, spokes)
+        ws.spin()
+        it = ws.spcomm.opt._PHIter if ws.strata_rank == 0 else -1
+        np.save(os.path.join(out_dir, f"r{rank}.npy"),
+                np.array([ws.BestInnerBound, ws.BestOuterBound, ws.strata_rank, ws.cylinder_rank, it,
+                          1.0 if ws.placement == "ranks" else 0.0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [3, 6])
+def test_wheel_on_separate_ranks(gpu, tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = np.array([np.load(tmp_path / f"r{k}.npy") for k in range(world)])
+    assert (r[:, 5] == 1).all()                                   # placement "ranks"
+    P = world // 3
+    assert list(r[:, 2]) == [c for c in range(3) for _ in range(P)]
+    ib, ob = r[0, 0], r[0, 1]
+    assert np.all(r[:, 0] == ib) and np.all(r[:, 1] == ob)        # everyone has the hub's bounds
+    assert ob <= FARMER_EF_OBJ + 1e-5 * abs(FARMER_EF_OBJ) <= ib + 2e-5 * abs(FARMER_EF_OBJ)
+    assert abs(ib - FARMER_EF_OBJ) <= 1e-4 * abs(FARMER_EF_OBJ), ib
+    assert (ib - ob) / abs(ob) <= 1e-4 + 1e-9                     # terminated on rel_gap
+    assert 1 <= r[0, 4] < 300
