@@ -285,7 +285,7 @@ def main():
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": a.warmup, "defaultPHrho": a.rho,
             "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
             "device": f"cuda:{dev_index}",
-            "iter0_solver_options": {"eps_rel": a.eps}, "iterk_solver_options": {"eps_rel": a.eps}}
+            "iterk_solver_options": {"eps_rel": a.eps}}
     t_setup = time.perf_counter()
     if a.model == "farmer":
         names = farmer.scenario_names_creator(a.scens)

@@ -15,6 +15,9 @@ from . import global_toc
 from .spopt import SPOpt
 
 
+LP_EPS_REL = 1e-10
+
+
 class PHBase(SPOpt):
     def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
                  all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None, extensions=None,
@@ -31,7 +34,13 @@ class PHBase(SPOpt):
         self.options_check()
         self.ph_converger = ph_converger
         self.rho_setter = rho_setter
-        self.iter0_solver_options = options.get("iter0_solver_options") or {}
+        # Iter0 solves pure LPs (W_on = prox_on = 0, phbase.py:594-597).  A first-order LP
+        # solution's x is only as accurate as the LP's sharpness allows (the KKT residuals
+        # bound the objective, not x), and that x seeds x̄ and W; so the LP default is one
+        # decade tighter than the prox QPs' (farmer cm = 64 needs it
+        # for W within 1e-5).  An explicit eps_rel in iter0_solver_options wins.
+        self.iter0_solver_options = dict(options.get("iter0_solver_options") or {})
+        self.iter0_solver_options.setdefault("eps_rel", LP_EPS_REL)
         self.iterk_solver_options = options.get("iterk_solver_options") or {}
         self.current_solver_options = self.iter0_solver_options
         self.convobject = None

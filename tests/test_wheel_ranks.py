@@ -4,7 +4,9 @@ windows of cylinders/transport.py.  Ranks are gloo processes sharing cuda:0 (1 o
 cylinder).  The asynchronous schedule changes the bound trajectory, so the check is on
 what does not depend on it: the outer bound is valid (<= the EF optimum), the inner
 bound reaches the EF optimum (test_sc.py:30-38: x* = 80/250/170, obj -108390), the gap
-closes to rel_gap, and every rank learns the same final bounds."""
+closes to rel_gap, and every rank learns the same final bounds.  The hub never waits for
+a spoke (as in the reference), so the iteration cap is set high enough that termination
+comes from the gap, however slowly the spokes run on the shared GPU."""
 import os
 import socket
 
@@ -41,8 +43,8 @@ def _worker(rank, world, port, out_dir):
         from mpisppy_amd.spin_the_wheel import WheelSpinner
         from mpisppy_amd.utils import cfg_vanilla as vanilla
         names = farmer.scenario_names_creator(3)
-        cfg = SimpleNamespace(solver_name="mi355x_pdhg", default_rho=1.0, max_iterations=300, rel_gap=1e-4,
-                              intra_hub_conv_thresh=1e-10, device="cuda:0", toc=False)
+        cfg = SimpleNamespace(solver_name="mi355x_pdhg", default_rho=1.0, max_iterations=20000, rel_gap=1e-4,
+                              intra_hub_conv_thresh=-1.0, device="cuda:0", toc=False)
         kw = {"num_scens": 3}
         hub = vanilla.ph_hub(cfg, farmer.scenario_creator, None, names, scenario_creator_kwargs=kw)
         spokes = [vanilla.lagrangian_spoke(cfg, farmer.scenario_creator, None, names, scenario_creator_kwargs=kw),
@@ -71,4 +73,4 @@ def test_wheel_on_separate_ranks(gpu, tmp_path, world):
     assert ob <= FARMER_EF_OBJ + 1e-5 * abs(FARMER_EF_OBJ) <= ib + 2e-5 * abs(FARMER_EF_OBJ)
     assert abs(ib - FARMER_EF_OBJ) <= 1e-4 * abs(FARMER_EF_OBJ), ib
     assert (ib - ob) / abs(ob) <= 1e-4 + 1e-9                     # terminated on rel_gap
-    assert 1 <= r[0, 4] < 300
+    assert 1 <= r[0, 4] < 20000
