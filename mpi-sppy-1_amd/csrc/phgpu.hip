@@ -77,6 +77,14 @@ struct phgpu_state {
     int wg_inst, wg_long;
     int32_t *wg_col_id, *wg_row_id, *wg_col_long, *wg_row_long, *wg_col_k, *wg_col_r, *wg_row_k, *wg_row_c;
     int default_kernel;  // 1 global, 2 register (L <= 64), 3 workgroup per scenario
+    // scenario-major records of the workgroup path: one contiguous record
+    // per scenario, so a workgroup loads / writes back its scenario in full lines
+    double* pk;
+    int64_t pk_stride;
+    int pk_A, pk_C, pk_Q, pk_DC, pk_LB, pk_UB, pk_RL, pk_RU, pk_DR, pk_RLH, pk_RUH, pk_X, pk_Y, pk_W, pk_RHO,
+        pk_XB;
+    int last_path;       // path of the last solve (whose layout holds the warm start)
+    int scen_set;
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
     // PH state (caller-owned)
@@ -246,6 +254,55 @@ __global__ void __launch_bounds__(BLOCK) k_setup(phgpu_state st, int ruiz_iters,
     // the reflected Halpern iteration diverge)
     st.normA[s] = lam > 0.0 ? 1.01 * sqrt(lam) : 1.0;
     st.omega[s] = 1.0;
+}
+
+// ------------------------------------------------------------------ record transposes
+// [K][S] (scenario-fastest, the C-ABI layout) <-> scenario-major records pk[s * stride +
+// off + k], through a 32 x 33 LDS tile so both sides are full-line accesses.
+#define TT 32
+__global__ void __launch_bounds__(256) k_to_records(const double* __restrict__ in, int K, int64_t S,
+                                                    double* __restrict__ pk, int64_t stride, int off) {
+    __shared__ double tile[TT][TT + 1];
+    const int64_t s0 = (int64_t)blockIdx.x * TT;
+    const int k0 = blockIdx.y * TT;
+    const int tx = threadIdx.x % TT, ty = threadIdx.x / TT;
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int k = k0 + r;
+        const int64_t s = s0 + tx;
+        tile[r][tx] = (k < K && s < S) ? in[(size_t)k * (size_t)S + (size_t)s] : 0.0;
+    }
+    __syncthreads();
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int64_t s = s0 + r;
+        const int k = k0 + tx;
+        if (s < S && k < K) pk[(size_t)s * (size_t)stride + off + k] = tile[tx][r];
+    }
+}
+
+// out[k][s] = pk[s][off + k] * (moff >= 0 ? pk[s][moff + k] : 1)
+__global__ void __launch_bounds__(256) k_from_records(const double* __restrict__ pk, int64_t stride, int off,
+                                                      int moff, int K, int64_t S, double* __restrict__ out) {
+    __shared__ double tile[TT][TT + 1];
+    const int64_t s0 = (int64_t)blockIdx.x * TT;
+    const int k0 = blockIdx.y * TT;
+    const int tx = threadIdx.x % TT, ty = threadIdx.x / TT;
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int64_t s = s0 + r;
+        const int k = k0 + tx;
+        double v = 0.0;
+        if (s < S && k < K) {
+            const size_t b = (size_t)s * (size_t)stride;
+            v = pk[b + off + k];
+            if (moff >= 0) v *= pk[b + moff + k];
+        }
+        tile[tx][r] = v;
+    }
+    __syncthreads();
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int k = k0 + r;
+        const int64_t s = s0 + tx;
+        if (k < K && s < S) out[(size_t)k * (size_t)S + (size_t)s] = tile[r][tx];
+    }
 }
 
 // ------------------------------------------------------------------ solve kernel
@@ -959,6 +1016,62 @@ static int dalloc(phgpu_state* h, T** p, size_t count) {
         if (rc_) { phgpu_destroy(h); return rc_; } \
     } while (0)
 
+// ---------------------------------------------------------- scenario-major records
+static hipError_t to_records(phgpu_state* h, const double* in, int K, int off, hipStream_t st) {
+    if (K <= 0) return hipSuccess;
+    const dim3 g((unsigned)((h->S + TT - 1) / TT), (unsigned)((K + TT - 1) / TT));
+    hipLaunchKernelGGL(k_to_records, g, dim3(256), 0, st, in, K, h->S, h->pk, h->pk_stride, off);
+    return hipGetLastError();
+}
+
+static hipError_t from_records(phgpu_state* h, int off, int moff, int K, double* out, hipStream_t st) {
+    if (K <= 0 || !out) return hipSuccess;
+    const dim3 g((unsigned)((h->S + TT - 1) / TT), (unsigned)((K + TT - 1) / TT));
+    hipLaunchKernelGGL(k_from_records, g, dim3(256), 0, st, (const double*)h->pk, h->pk_stride, off, moff, K,
+                       h->S, out);
+    return hipGetLastError();
+}
+
+// record layout: A (CSR order) | c q Dc lb^ ub^ (n) | rl ru Dr rl^ ru^ (m) | x^ (n) y^ (m)
+// warm start | W rho xbar (nn) PH state of the current solve; stride rounded to 16 doubles
+static int pack_alloc(phgpu_state* h) {
+    if (h->pk) return 0;
+    const int n = h->n, m = h->m, nnz = h->nnz, nn = h->nn;
+    int o = 0;
+    h->pk_A = o; o += nnz;
+    h->pk_C = o; o += n;
+    h->pk_Q = o; o += n;
+    h->pk_DC = o; o += n;
+    h->pk_LB = o; o += n;
+    h->pk_UB = o; o += n;
+    h->pk_RL = o; o += m;
+    h->pk_RU = o; o += m;
+    h->pk_DR = o; o += m;
+    h->pk_RLH = o; o += m;
+    h->pk_RUH = o; o += m;
+    h->pk_X = o; o += n;
+    h->pk_Y = o; o += m;
+    h->pk_W = o; o += nn;
+    h->pk_RHO = o; o += nn;
+    h->pk_XB = o; o += nn;
+    h->pk_stride = (o + 15) / 16 * 16;
+    return dalloc(h, &h->pk, (size_t)h->pk_stride * (size_t)h->S);
+}
+
+// copy the scaled problem (k_setup's output) into the records
+static hipError_t pack_fill(phgpu_state* h, hipStream_t st) {
+    struct { const double* a; int K, off; } f[] = {
+        {h->Ah_csr, h->nnz, h->pk_A}, {h->c, h->n, h->pk_C}, {h->q, h->n, h->pk_Q}, {h->Dc, h->n, h->pk_DC},
+        {h->lbh, h->n, h->pk_LB}, {h->ubh, h->n, h->pk_UB}, {h->rl, h->m, h->pk_RL}, {h->ru, h->m, h->pk_RU},
+        {h->Dr, h->m, h->pk_DR}, {h->rlh, h->m, h->pk_RLH}, {h->ruh, h->m, h->pk_RUH}, {h->x, h->n, h->pk_X},
+        {h->y, h->m, h->pk_Y}};
+    for (auto& e : f) {
+        const hipError_t r = to_records(h, e.a, e.K, e.off, st);
+        if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+}
+
 extern "C" int phgpu_default_options(phgpu_options* o) {
     if (!o) return set_err(-1, "null options");
     o->eps_rel = 1e-9;
@@ -1233,6 +1346,13 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
         if (h->reg_inst >= 0 && (h->wg_inst < 0 || reg_cost_s <= best)) h->default_kernel = 2;
         else if (h->wg_inst >= 0) h->default_kernel = 3;
         else h->default_kernel = 1;
+        if (h->default_kernel == 3) {
+            const int rc3 = pack_alloc(h);
+            if (rc3) {
+                phgpu_destroy(h);
+                return rc3;
+            }
+        }
     }
     *out = h;
     return 0;
@@ -1269,7 +1389,10 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_setup, grid_for(h->S), dim3(BLOCK), 0, st, *h, 10, 200);
     HIPCHK(hipGetLastError());
+    if (h->pk) HIPCHK(pack_fill(h, st));
     h->have_solution = 0;
+    h->scen_set = 1;
+    h->last_path = 0;
     return 0;
 }
 
@@ -1330,6 +1453,26 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         return set_err(-1, "register-resident kernels require gamma = 1 (got %g)", o.gamma);
     const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? h->default_kernel : 1);
     const bool use_reg = path == 2;
+    if (path == 3 && !h->pk) {
+        const int rc3 = pack_alloc(h);
+        if (rc3) return rc3;
+        if (h->scen_set) HIPCHK(pack_fill(h, st));
+    }
+    if (path == 3) {
+        // this solve's PH state into the records; a warm start left by another path too
+        if (h->W_on) HIPCHK(to_records(h, h->W, h->nn, h->pk_W, st));
+        if (h->prox_on) {
+            HIPCHK(to_records(h, h->rho, h->nn, h->pk_RHO, st));
+            HIPCHK(to_records(h, h->xbar, h->nn, h->pk_XB, st));
+        }
+        if (P.warm && h->last_path != 3) {
+            HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
+            HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
+        }
+    } else if (P.warm && h->last_path == 3) {
+        HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
+        HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
+    }
     if (path == 3) {
         const wg_instance& gi = g_wg_instances[h->wg_inst];
         wg_plan pl;
@@ -1355,6 +1498,10 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
         hipLaunchKernelGGL(gi.fn, dim3((unsigned)nblk), dim3(pl.L), lds, st, *h, P, pl, h->qhead, x, y, obj, bound,
                            status, iters);
+        HIPCHK(hipGetLastError());
+        // outputs in the caller's scenario-fastest layout, unscaled
+        HIPCHK(from_records(h, h->pk_X, h->pk_DC, h->n, x, st));
+        if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
     } else if (use_reg) {
         reg_plan pl;
         pl.L = h->reg_L;
@@ -1387,6 +1534,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     }
     HIPCHK(hipGetLastError());
     h->have_solution = 1;
+    h->last_path = path;
     return 0;
 }
 
@@ -1437,6 +1585,10 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_fix_nonants, grid_for(h->S), dim3(BLOCK), 0, st, *h, xfix);
     HIPCHK(hipGetLastError());
+    if (h->pk) {
+        HIPCHK(to_records(h, h->lbh, h->n, h->pk_LB, st));
+        HIPCHK(to_records(h, h->ubh, h->n, h->pk_UB, st));
+    }
     return 0;
 }
 
@@ -1449,7 +1601,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->rlh, h->ruh, h->ch, h->qh, h->x, h->x0, h->xe, h->xt, h->aty, h->aty0,
                     h->y, h->y0, h->yt, h->omega, h->part, h->part_node, h->pl_col_k,
                     h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead, h->wg_col_id, h->wg_row_id,
-                    h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c};
+                    h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c,
+                    h->pk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
