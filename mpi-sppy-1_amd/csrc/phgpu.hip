@@ -912,10 +912,14 @@ static inline long slot_cost(int KC, int ZC, int KR, int ZR, int nlong) {
     return (long)KC * (10 + 2 * ZC) + (long)KR * (8 + 2 * ZR) + 20L * nlong;
 }
 
+// The workgroup kernels spill only around a scenario's load and write-back (the solve
+// loops of every instance are scratch-free: objdump of the code object), once per
+// several hundred PDHG iterations, so their cap is looser than the register path's.
+#define WG_SPILL_MAX 512
 static bool wg_spills(const wg_instance& g) {
     hipFuncAttributes a;
     if (hipFuncGetAttributes(&a, (const void*)g.fn) != hipSuccess) return false;
-    return a.localSizeBytes > REG_SPILL_MAX;
+    return a.localSizeBytes > WG_SPILL_MAX;
 }
 
 struct wg_plan_host {
@@ -1100,7 +1104,8 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
                             int32_t nlen_max) {
     if (!out) return set_err(-1, "null handle pointer");
     *out = nullptr;
-    if (S <= 0 || n <= 0 || m < 0 || nnz < 0 || nn < 0 || depth < 1 || num_nodes < 1 || nlen_max < 0)
+    if (S <= 0 || S >= (1LL << 31) || n <= 0 || m < 0 || nnz < 0 || nn < 0 || depth < 1 || num_nodes < 1 ||
+        nlen_max < 0)
         return set_err(-1, "bad sizes S=%lld n=%d m=%d nnz=%d nn=%d depth=%d nodes=%d",
                        (long long)S, n, m, nnz, nn, depth, num_nodes);
     if (!row_ptr || (nnz > 0 && !col_idx) || (nn > 0 && (!nonant_col || !nonant_depth || !nonant_off)))
