@@ -29,7 +29,8 @@
  *   - Per-scenario arrays are scenario-fastest: element (k, s) of a k-indexed
  *     quantity lives at [k * S + s]  (coalesced: 64 lanes = 64 scenarios).
  *   - All work is ordered on the given hipStream_t (NULL = default stream); no call
- *     synchronises the device except phgpu_create / phgpu_destroy.
+ *     synchronises the device except phgpu_create / phgpu_destroy and
+ *     phgpu_set_scenarios on a shared-matrix handle (it sizes its records from the data).
  *   - A handle is used by one host thread; it is not re-entrant; one process per GPU.
  *   - The problem is stored as a minimisation; a maximise model is negated by the
  *     caller (phbase.py:696-699 subtracts the PH term for max, which is the same).
@@ -77,7 +78,9 @@ typedef struct {
     double omega_clamp;    /* primal weight kept in [1/clamp, clamp] (scaled) [1e4] */
     int32_t kernel;        /* 0 auto, 1 global-memory kernel, 2 register-resident
                               kernel (error if no compiled instance fits),
-                              3 workgroup-per-scenario kernel (large scenarios) [0] */
+                              3 workgroup-per-scenario kernel (large scenarios),
+                              4 shared-matrix streaming kernel (the only path, and
+                              the automatic one, of a PHGPU_SHARED_MATRIX handle) [0] */
     int32_t infeas_start;  /* infeasibility certificates are tested at the KKT
                               checks from this iteration on (< 0: never)      [512] */
     double eps_infeas;     /* certificate tolerance: ray violation <= eps * |ray
@@ -107,8 +110,25 @@ int phgpu_create(phgpu_handle* h, int device, int64_t S, int32_t n, int32_t m, i
                  const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
                  int32_t nlen_max);
 
+/* Flags of phgpu_create2.
+ * PHGPU_SHARED_MATRIX: every scenario has the same constraint-matrix values (the UC
+ *   relaxation: scenarios differ in bounds only).  phgpu_set_scenarios then takes
+ *   A_val[nnz] (one copy), scales it once, and keeps per scenario only the iterates and
+ *   the columns / rows whose data differ between scenarios (plus the nonant columns);
+ *   solves run on path 4 (one workgroup streams one scenario).  Meant for
+ *   scenarios too large for the register / workgroup-resident paths. */
+#define PHGPU_SHARED_MATRIX 1u
+
+/* phgpu_create with flags (phgpu_create(...) == phgpu_create2(..., 0)). */
+int phgpu_create2(phgpu_handle* h, int device, int64_t S, int32_t n, int32_t m, int32_t nnz,
+                  const int32_t* row_ptr, const int32_t* col_idx, int32_t nn,
+                  const int32_t* nonant_col, const int32_t* nonant_depth,
+                  const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
+                  int32_t nlen_max, uint32_t flags);
+
 /* Upload per-scenario data (device pointers, scenario-fastest):
- *   A_val[nnz*S], c/lb/ub/q[n*S] (q may be NULL = 0), rl/ru[m*S] (+-inf allowed),
+ *   A_val[nnz*S] (A_val[nnz] on a PHGPU_SHARED_MATRIX handle), c/lb/ub/q[n*S]
+ *   (q may be NULL = 0), rl/ru[m*S] (+-inf allowed),
  *   obj_const[S] (may be NULL), prob[S], node_of[depth*S] (int32 global node id),
  *   prob_coeff[depth*S] (pi_s / pi_node, spbase.py:384-391).
  * Computes the diagonal (Ruiz + Pock-Chambolle) scaling and ||A_scaled||_2 per
@@ -187,7 +207,8 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  * {register path (L <= 64 lanes per scenario): instance or -1, L, column slots / CSC
  *  entries per column / row slots / CSR entries per row needed, the instance's KC, ZC, KR,
  *  ZR;  workgroup path (one workgroup per scenario): instance or -1, waves per scenario,
- *  KC, ZC, KR, ZR;  the default path of phgpu_solve: 1 global, 2 register, 3 workgroup}. */
+ *  KC, ZC, KR, ZR;  the default path of phgpu_solve: 1 global, 2 register, 3 workgroup,
+ *  4 shared-matrix streaming}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
 #ifdef __cplusplus

@@ -87,6 +87,16 @@ struct phgpu_state {
     int scen_set;
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
+    // shared-matrix handle (PHGPU_SHARED_MATRIX, path 4: solve_stream.inc): one scaled A
+    // (A / Ah_csr / Ah_csc [nnz], Dr [m], Dc [n]) for all scenarios; the shared base of
+    // the column / row data (sh_col: ch qh lbh ubh, sh_row: rlh ruh rl ru, scenario 0);
+    // per-scenario columns P (cmap[j] = index or -1, pcol) and rows R (rmap, prow)
+    int shared;
+    int np, nr;
+    int32_t *cmap, *rmap, *pcol, *prow;
+    double *sh_col, *sh_row, *sh_norm, *sh_v, *sh_u, *sh_w, *sh_part;
+    double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
+    int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
     // PH state (caller-owned)
     const double *W, *rho, *xbar;
     int W_on, prox_on;
@@ -589,6 +599,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 
 #include "solve_reg.inc"
 #include "solve_wg.inc"
+#include "solve_stream.inc"
 
 // ------------------------------------------------------------------ PH reductions
 // phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
@@ -1102,6 +1113,16 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
                             int32_t nn, const int32_t* nonant_col, const int32_t* nonant_depth,
                             const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
                             int32_t nlen_max) {
+    return phgpu_create2(out, device, S, n, m, nnz, row_ptr, col_idx, nn, nonant_col, nonant_depth, nonant_off,
+                         depth, num_nodes, nlen_max, 0u);
+}
+
+extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n, int32_t m,
+                             int32_t nnz, const int32_t* row_ptr, const int32_t* col_idx,
+                             int32_t nn, const int32_t* nonant_col, const int32_t* nonant_depth,
+                             const int32_t* nonant_off, int32_t depth, int32_t num_nodes,
+                             int32_t nlen_max, uint32_t flags) {
+    if (flags & ~(uint32_t)PHGPU_SHARED_MATRIX) return set_err(-1, "unknown flags 0x%x", flags);
     if (!out) return set_err(-1, "null handle pointer");
     *out = nullptr;
     if (S <= 0 || S >= (1LL << 31) || n <= 0 || m < 0 || nnz < 0 || nn < 0 || depth < 1 || num_nodes < 1 ||
@@ -1175,38 +1196,58 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
     ALLOC(h->nonant_depth, nn);
     ALLOC(h->nonant_off, nn);
     ALLOC(h->nonant_slot, n);
-    ALLOC(h->A, (size_t)nnz * Sz);
-    ALLOC(h->c, (size_t)n * Sz);
-    ALLOC(h->lb, (size_t)n * Sz);
-    ALLOC(h->ub, (size_t)n * Sz);
-    ALLOC(h->q, (size_t)n * Sz);
-    ALLOC(h->rl, (size_t)m * Sz);
-    ALLOC(h->ru, (size_t)m * Sz);
     ALLOC(h->objc, Sz);
     ALLOC(h->prob, Sz);
     ALLOC(h->pcoef, (size_t)depth * Sz);
     ALLOC(h->node_of, (size_t)depth * Sz);
-    ALLOC(h->Ah_csr, (size_t)nnz * Sz);
-    ALLOC(h->Ah_csc, (size_t)nnz * Sz);
-    ALLOC(h->Dr, (size_t)m * Sz);
-    ALLOC(h->Dc, (size_t)n * Sz);
-    ALLOC(h->normA, Sz);
-    ALLOC(h->lbh, (size_t)n * Sz);
-    ALLOC(h->ubh, (size_t)n * Sz);
-    ALLOC(h->rlh, (size_t)m * Sz);
-    ALLOC(h->ruh, (size_t)m * Sz);
-    ALLOC(h->ch, (size_t)n * Sz);
-    ALLOC(h->qh, (size_t)n * Sz);
-    ALLOC(h->x, (size_t)n * Sz);
-    ALLOC(h->x0, (size_t)n * Sz);
-    ALLOC(h->xe, (size_t)n * Sz);
-    ALLOC(h->xt, (size_t)n * Sz);
-    ALLOC(h->aty, (size_t)n * Sz);
-    ALLOC(h->aty0, (size_t)n * Sz);
-    ALLOC(h->y, (size_t)m * Sz);
-    ALLOC(h->y0, (size_t)m * Sz);
-    ALLOC(h->yt, (size_t)m * Sz);
     ALLOC(h->omega, Sz);
+    h->shared = (flags & PHGPU_SHARED_MATRIX) ? 1 : 0;
+    if (h->shared) {
+        // one scaled matrix; iterates and per-scenario data live in the stream records
+        // (allocated by phgpu_set_scenarios once the per-scenario column set is known)
+        ALLOC(h->A, nnz);
+        ALLOC(h->Ah_csr, nnz);
+        ALLOC(h->Ah_csc, nnz);
+        ALLOC(h->Dr, m);
+        ALLOC(h->Dc, n);
+        ALLOC(h->cmap, n);
+        ALLOC(h->rmap, m);
+        ALLOC(h->sh_col, 4 * (size_t)n);
+        ALLOC(h->sh_row, 4 * (size_t)m);
+        ALLOC(h->sh_norm, 4);
+        ALLOC(h->sh_v, n);
+        ALLOC(h->sh_u, n);
+        ALLOC(h->sh_w, m);
+        ALLOC(h->sh_part, (size_t)(n + 255) / 256 + 1);
+    } else {
+        ALLOC(h->A, (size_t)nnz * Sz);
+        ALLOC(h->c, (size_t)n * Sz);
+        ALLOC(h->lb, (size_t)n * Sz);
+        ALLOC(h->ub, (size_t)n * Sz);
+        ALLOC(h->q, (size_t)n * Sz);
+        ALLOC(h->rl, (size_t)m * Sz);
+        ALLOC(h->ru, (size_t)m * Sz);
+        ALLOC(h->Ah_csr, (size_t)nnz * Sz);
+        ALLOC(h->Ah_csc, (size_t)nnz * Sz);
+        ALLOC(h->Dr, (size_t)m * Sz);
+        ALLOC(h->Dc, (size_t)n * Sz);
+        ALLOC(h->normA, Sz);
+        ALLOC(h->lbh, (size_t)n * Sz);
+        ALLOC(h->ubh, (size_t)n * Sz);
+        ALLOC(h->rlh, (size_t)m * Sz);
+        ALLOC(h->ruh, (size_t)m * Sz);
+        ALLOC(h->ch, (size_t)n * Sz);
+        ALLOC(h->qh, (size_t)n * Sz);
+        ALLOC(h->x, (size_t)n * Sz);
+        ALLOC(h->x0, (size_t)n * Sz);
+        ALLOC(h->xe, (size_t)n * Sz);
+        ALLOC(h->xt, (size_t)n * Sz);
+        ALLOC(h->aty, (size_t)n * Sz);
+        ALLOC(h->aty0, (size_t)n * Sz);
+        ALLOC(h->y, (size_t)m * Sz);
+        ALLOC(h->y0, (size_t)m * Sz);
+        ALLOC(h->yt, (size_t)m * Sz);
+    }
     ALLOC(h->qhead, 1);
     {
         int ncu = 0;
@@ -1247,6 +1288,12 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
     // and past any L whose instance spills (reg_spills);
     // PHGPU_LANES=<L> pins it (tuning / tests)
     h->reg_inst = -1;
+    h->wg_inst = -1;
+    if (h->shared) {
+        h->default_kernel = 4;
+        *out = h;
+        return 0;
+    }
     {
         const int64_t target = (int64_t)h->num_cus * 4 * WAVE * REG_WAVES_PER_EU;
         const char* env = getenv("PHGPU_LANES");
@@ -1365,6 +1412,121 @@ extern "C" int phgpu_create(phgpu_handle* out, int device, int64_t S, int32_t n,
 
 static inline dim3 grid_for(int64_t S) { return dim3((unsigned)((S + BLOCK - 1) / BLOCK)); }
 
+// phgpu_set_scenarios on a shared-matrix handle: A_val holds nnz values (one copy for
+// all scenarios).  Scales A once, finds the columns / rows whose data differ between
+// scenarios (plus every nonant column), sizes the stream records and fills them.  Sizing
+// the records needs those counts on the host: this call synchronises the stream once.
+static int set_scenarios_shared(phgpu_state* h, const double* A_val, const double* c, const double* lb,
+                                const double* ub, const double* rl, const double* ru, const double* q,
+                                const double* obj_const, const double* prob, const int32_t* node_of,
+                                const double* prob_coeff, hipStream_t st) {
+    const size_t Sz = (size_t)h->S;
+    const int n = h->n, m = h->m, nnz = h->nnz;
+    auto cp = [&](double* dst, const double* src, size_t cnt) -> hipError_t {
+        if (cnt == 0) return hipSuccess;
+        return hipMemcpyAsync(dst, src, cnt * sizeof(double), hipMemcpyDeviceToDevice, st);
+    };
+    HIPCHK(cp(h->A, A_val, (size_t)nnz));
+    if (obj_const) HIPCHK(cp(h->objc, obj_const, Sz));
+    else HIPCHK(hipMemsetAsync(h->objc, 0, Sz * sizeof(double), st));
+    HIPCHK(cp(h->prob, prob, Sz));
+    HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
+    HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    const int big = std::max(nnz, std::max(n, m));
+    const dim3 gb((unsigned)((big + 255) / 256)), gn((unsigned)((n + 255) / 256)), gm((unsigned)((m + 255) / 256));
+    const dim3 gz((unsigned)((nnz + 255) / 256 > 0 ? (nnz + 255) / 256 : 1));
+    // Ruiz (10 max passes) + Pock-Chambolle (sum) pass, as k_setup
+    hipLaunchKernelGGL(k_sh_init, gb, dim3(256), 0, st, *h);
+    for (int pass = 0; pass <= 10; ++pass) {
+        const int pc = pass == 10;
+        if (m) hipLaunchKernelGGL(k_sh_rowfac, gm, dim3(256), 0, st, *h, pc, h->sh_w);
+        hipLaunchKernelGGL(k_sh_colfac, gn, dim3(256), 0, st, *h, pc, h->sh_u);
+        hipLaunchKernelGGL(k_sh_apply, gb, dim3(256), 0, st, *h, (const double*)h->sh_w, (const double*)h->sh_u);
+    }
+    hipLaunchKernelGGL(k_sh_csc, gz, dim3(256), 0, st, *h);
+    // ||A_scaled||_2: 200 power iterations on A^T A
+    hipLaunchKernelGGL(k_sh_vinit, gn, dim3(256), 0, st, *h, h->sh_v);
+    for (int it = 0; it < 200; ++it) {
+        if (m) hipLaunchKernelGGL(k_sh_rowmv, gm, dim3(256), 0, st, *h, (const double*)h->sh_v, h->sh_w);
+        hipLaunchKernelGGL(k_sh_colmv, gn, dim3(256), 0, st, *h, (const double*)h->sh_w, h->sh_u, h->sh_part);
+        hipLaunchKernelGGL(k_sh_norm, dim3(1), dim3(256), 0, st, (const double*)h->sh_part, (int)gn.x, h->sh_norm + 3);
+        hipLaunchKernelGGL(k_sh_normalize, gn, dim3(256), 0, st, *h, (const double*)h->sh_u,
+                           (const double*)(h->sh_norm + 3), h->sh_v);
+    }
+    hipLaunchKernelGGL(k_sh_finish_norm, dim3(1), dim3(1), 0, st, *h);
+    hipLaunchKernelGGL(k_sh_base, gb, dim3(256), 0, st, *h, c, q, lb, ub, rl, ru);
+    HIPCHK(hipGetLastError());
+    // which columns / rows differ between scenarios (one wave per entry)
+    int32_t* flags = nullptr;
+    HIPCHK(hipMalloc((void**)&flags, (size_t)(n + m + 1) * sizeof(int32_t)));
+    hipLaunchKernelGGL(k_sh_vary, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, c, q, lb, ub, n, h->S, flags);
+    if (m) hipLaunchKernelGGL(k_sh_vary, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, st, rl, ru, (const double*)nullptr,
+                              (const double*)nullptr, m, h->S, flags + n);
+    HIPCHK(hipGetLastError());
+    std::vector<int32_t> fl((size_t)n + m + 1, 0), slot((size_t)n, -1);
+    HIPCHK(hipMemcpyAsync(fl.data(), flags, (size_t)(n + m) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(slot.data(), h->nonant_slot, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipFree(flags));
+    std::vector<int32_t> cmap((size_t)n, -1), rmap((size_t)m + 1, -1), pcol, prow;
+    for (int j = 0; j < n; ++j)
+        if (fl[j] || slot[j] >= 0) {
+            cmap[j] = (int32_t)pcol.size();
+            pcol.push_back(j);
+        }
+    for (int i = 0; i < m; ++i)
+        if (fl[(size_t)n + i]) {
+            rmap[i] = (int32_t)prow.size();
+            prow.push_back(i);
+        }
+    h->np = (int)pcol.size();
+    h->nr = (int)prow.size();
+    if (h->pcol) HIPCHK(hipFree(h->pcol));
+    if (h->prow) HIPCHK(hipFree(h->prow));
+    h->pcol = h->prow = nullptr;
+    if (dalloc(h, &h->pcol, pcol.size()) || dalloc(h, &h->prow, prow.size())) return -3;
+    HIPCHK(hipMemcpy(h->cmap, cmap.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (m) HIPCHK(hipMemcpy(h->rmap, rmap.data(), (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!pcol.empty()) HIPCHK(hipMemcpy(h->pcol, pcol.data(), pcol.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!prow.empty()) HIPCHK(hipMemcpy(h->prow, prow.data(), prow.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    // record layout, every part aligned to 16 doubles (128 B)
+    auto al = [](int64_t v) { return (v + 15) / 16 * 16; };
+    int64_t o = 0;
+    h->sk_X = o; o += al(n);
+    h->sk_X0 = o; o += al(n);
+    h->sk_U = o; o += al(n);
+    h->sk_XT = o; o += al(n);
+    h->sk_Y = o; o += al(m);
+    h->sk_Y0 = o; o += al(m);
+    h->sk_YT = o; o += al(m);
+    h->sk_PC = o; o += al(8 * (int64_t)h->np);
+    h->sk_PR = o; o += al(4 * (int64_t)h->nr);
+    h->sk_stride = o;
+    const int64_t need = o * h->S;
+    if (need > h->sk_cap) {
+        if (h->sk) {
+            HIPCHK(hipFree(h->sk));
+            h->ws_bytes -= h->sk_cap * (int64_t)sizeof(double);
+            h->sk = nullptr;
+        }
+        const int rc = dalloc(h, &h->sk, (size_t)need);
+        if (rc) return rc;
+        h->sk_cap = need;
+    }
+    const int64_t per = (int64_t)h->np + h->nr;
+    if (per > 0) {
+        const int64_t tot = per * h->S;
+        hipLaunchKernelGGL(k_sh_fill, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, *h, c, q, lb, ub, rl, ru);
+    }
+    hipLaunchKernelGGL(k_sh_normbase, dim3(1), dim3(256), 0, st, *h, c, rl, ru);
+    hipLaunchKernelGGL(k_sh_fill_omega, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
+    HIPCHK(hipGetLastError());
+    h->have_solution = 0;
+    h->scen_set = 1;
+    h->last_path = 0;
+    return 0;
+}
+
 extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
                                    const double* lb, const double* ub, const double* rl,
                                    const double* ru, const double* q, const double* obj_const,
@@ -1374,6 +1536,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     if ((h->nnz && !A_val) || !c || !lb || !ub || (h->m && (!rl || !ru)) || !prob || !node_of || !prob_coeff)
         return set_err(-1, "null scenario array");
     hipStream_t st = (hipStream_t)stream;
+    if (h->shared) return set_scenarios_shared(h, A_val, c, lb, ub, rl, ru, q, obj_const, prob, node_of, prob_coeff, st);
     const size_t Sz = (size_t)h->S;
     auto cp = [&](double* dst, const double* src, size_t cnt) -> hipError_t {
         if (cnt == 0) return hipSuccess;
@@ -1449,7 +1612,25 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     hipStream_t st = (hipStream_t)stream;
     // the register-resident kernels are specialised for the reflected step (gamma = 1, the
     // default); another gamma runs on the global-memory kernel
-    if (o.kernel < 0 || o.kernel > 3) return set_err(-1, "bad kernel option %d", o.kernel);
+    if (o.kernel < 0 || o.kernel > 4) return set_err(-1, "bad kernel option %d", o.kernel);
+    if (h->shared != (o.kernel == 4 || (o.kernel == 0 && h->shared)))
+        return set_err(-1, "kernel option %d: a shared-matrix handle solves with path 4 only (kernel 0 or 4), "
+                       "other handles with paths 1-3", o.kernel);
+    if (h->shared) {
+        if (!h->scen_set) return set_err(-1, "phgpu_set_scenarios has not been called");
+        int per_cu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_solve_stream, SBLK, 0));
+        if (per_cu < 1) per_cu = 1;
+        int64_t nblk = (int64_t)per_cu * h->num_cus;
+        if (nblk > h->S) nblk = h->S;
+        HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
+        hipLaunchKernelGGL(k_solve_stream, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj, bound,
+                           status, iters);
+        HIPCHK(hipGetLastError());
+        h->have_solution = 1;
+        h->last_path = 4;
+        return 0;
+    }
     if (o.kernel == 2 && h->reg_inst < 0)
         return set_err(-1, "register-resident kernel requested but no compiled instance fits this pattern");
     if (o.kernel == 3 && h->wg_inst < 0)
@@ -1588,6 +1769,12 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
     if (!h) return set_err(-1, "null handle");
     if (h->nn == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    if (h->shared) {
+        const int64_t tot = (int64_t)h->nn * h->S;
+        hipLaunchKernelGGL(k_fix_nonants_sh, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, *h, xfix);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     hipLaunchKernelGGL(k_fix_nonants, grid_for(h->S), dim3(BLOCK), 0, st, *h, xfix);
     HIPCHK(hipGetLastError());
     if (h->pk) {
@@ -1607,7 +1794,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->y, h->y0, h->yt, h->omega, h->part, h->part_node, h->pl_col_k,
                     h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead, h->wg_col_id, h->wg_row_id,
                     h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c,
-                    h->pk};
+                    h->pk, h->cmap, h->rmap, h->pcol, h->prow, h->sh_col, h->sh_row, h->sh_norm, h->sh_v,
+                    h->sh_u, h->sh_w, h->sh_part, h->sk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;

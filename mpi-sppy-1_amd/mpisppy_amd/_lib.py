@@ -40,9 +40,10 @@ class PhgpuOptions(ctypes.Structure):
 
 
 OPTIMAL, ITER_LIMIT, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE = 0, 1, 2, 3
+SHARED_MATRIX = 1          # phgpu_create2 flag (include/phgpu.h)
 
 # every symbol include/phgpu.h declares (tests check the library exports them all)
-EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_set_scenarios", "phgpu_set_ph_state",
+EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_scenarios", "phgpu_set_ph_state",
            "phgpu_solve", "phgpu_ph_reduce", "phgpu_ph_update", "phgpu_expectations",
            "phgpu_fix_nonants", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info"]
@@ -67,6 +68,7 @@ def load(path=None):
     lib.phgpu_default_options.argtypes = [ctypes.POINTER(PhgpuOptions)]
     lib.phgpu_create.argtypes = [ctypes.POINTER(c_vp), c_int, c_i64, c_i32, c_i32, c_i32, P_i32,
                                  P_i32, c_i32, P_i32, P_i32, P_i32, c_i32, c_i32, c_i32]
+    lib.phgpu_create2.argtypes = lib.phgpu_create.argtypes + [ctypes.c_uint32]
     lib.phgpu_set_scenarios.argtypes = [c_vp] + [c_vp] * 11 + [c_vp]
     lib.phgpu_set_ph_state.argtypes = [c_vp, c_vp, c_vp, c_vp, c_int, c_int]
     lib.phgpu_solve.argtypes = [c_vp, ctypes.POINTER(PhgpuOptions), c_int, c_vp, c_vp, c_vp, c_vp,

@@ -171,6 +171,33 @@ def fold_singleton_rows(row_ptr, col_idx, A_val, lb, ub, rl, ru):
     return (new_ptr, col_idx[ent_keep], A_val[:, ent_keep], lb, ub, rl[:, keep], ru[:, keep], keep)
 
 
+def drop_duplicate_rows(row_ptr, col_idx, A_val, rl, ru):
+    """Drop rows that repeat an earlier row exactly (same columns, same coefficients
+    and same range in every scenario).  The feasible set is unchanged.  The UC model
+    declares its production-cost row once per piecewise segment
+    (ReferenceModel_OK.py:1466-1470: indexed by (g, t, i), the body does not use i),
+    which would otherwise add ~15k redundant rows and ~40% of the nonzeros.  Returns
+    the reduced arrays and the kept-row mask."""
+    m = rl.shape[1]
+    keep = np.ones(m, dtype=bool)
+    seen = {}
+    for r in range(m):
+        a, b = row_ptr[r], row_ptr[r + 1]
+        if b == a:
+            continue
+        key = (col_idx[a:b].tobytes(), A_val[:, a:b].tobytes(), rl[:, r].tobytes(), ru[:, r].tobytes())
+        if key in seen:
+            keep[r] = False
+        else:
+            seen[key] = r
+    if keep.all():
+        return row_ptr, col_idx, A_val, rl, ru, keep
+    counts = np.diff(row_ptr)
+    ent_keep = np.repeat(keep, counts)
+    new_ptr = np.concatenate([[0], np.cumsum(counts[keep])]).astype(np.int32)
+    return new_ptr, col_idx[ent_keep], A_val[:, ent_keep], rl[:, keep], ru[:, keep], keep
+
+
 # ---------------------------------------------------------------- from models
 def _nonleaf_node_ids(models, all_nodenames):
     """Global node ids (index into the nonleaf node list) in all_nodenames order."""
@@ -235,6 +262,7 @@ def batch_from_models(names, models, all_nodenames=None, num_all_scens=None, pre
     if presolve:
         row_ptr, col_idx, A_val, lb, ub, rl, ru, _ = fold_singleton_rows(row_ptr, col_idx, A_val,
                                                                         lb, ub, rl, ru)
+        row_ptr, col_idx, A_val, rl, ru, _ = drop_duplicate_rows(row_ptr, col_idx, A_val, rl, ru)
     # nonants / tree (spbase.py:293-320, 378-391)
     if node_names is None:
         node_names = _nonleaf_node_ids(models, all_nodenames)

@@ -36,8 +36,23 @@ def combine_node_partials(comm, node_buf):
     return comm.allreduce_sum_(node_buf)
 
 
+# scenarios at least this large (n + m) whose matrix values are the same in every
+# scenario run on the shared-matrix streaming path (path 4, include/phgpu.h
+# PHGPU_SHARED_MATRIX); smaller ones fit the register / workgroup-resident paths
+SHARED_MIN_SIZE = 8192
+
+
+def matrix_is_shared(batch):
+    """True if every scenario of the batch has the same constraint-matrix values."""
+    A = batch.A_val
+    return A.shape[0] <= 1 or (A.strides[0] == 0) or bool(np.all(A == A[:1]))
+
+
 class PHEngine:
-    def __init__(self, batch, device=None, comm=None, node_names=None):
+    def __init__(self, batch, device=None, comm=None, node_names=None, shared=None):
+        """``shared``: None = the shared-matrix path when the matrix is the same in every
+        scenario and the scenarios are large (SHARED_MIN_SIZE); True / False force it
+        (True requires the same matrix)."""
         if not torch.cuda.is_available():
             raise _lib.PhgpuError("PHEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = _lib.load()
@@ -65,13 +80,19 @@ class PHEngine:
         nd = np.ascontiguousarray(b.nonant_depth, dtype=np.int32)
         no = np.ascontiguousarray(b.nonant_off, dtype=np.int32)
         P = lambda a: a.ctypes.data_as(_lib.P_i32)  # noqa: E731
+        if shared is None:
+            shared = (n + m) >= SHARED_MIN_SIZE and matrix_is_shared(b)
+        elif shared and not matrix_is_shared(b):
+            raise ValueError("shared=True needs the same matrix values in every scenario")
+        self.shared = bool(shared)
         torch.cuda.set_device(self.dev_index)
-        _lib.check(self.lib.phgpu_create(ctypes.byref(h), self.dev_index, S, n, m, b.nnz, P(rp), P(ci),
-                                         nn, P(nc), P(nd), P(no), b.depth, self.num_nodes,
-                                         self.nlen_max), "phgpu_create")
+        _lib.check(self.lib.phgpu_create2(ctypes.byref(h), self.dev_index, S, n, m, b.nnz, P(rp), P(ci),
+                                          nn, P(nc), P(nd), P(no), b.depth, self.num_nodes,
+                                          self.nlen_max, _lib.SHARED_MATRIX if self.shared else 0),
+                   "phgpu_create2")
         self.h = h
         dev = self.device
-        self.A_val = _dev_T(b.A_val, dev)
+        self.A_val = _dev_T(b.A_val[0] if self.shared else b.A_val, dev)
         self.c = _dev_T(b.c, dev)
         self.lb = _dev_T(b.lb, dev)
         self.ub = _dev_T(b.ub, dev)

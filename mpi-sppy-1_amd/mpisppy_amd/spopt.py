@@ -43,7 +43,7 @@ class SPOpt(SPBase):
             raise RuntimeError(f"solver_name {sname!r} is not served by this engine; use one of {SOLVER_NAMES}")
         if self.engine is None:
             self.engine = PHEngine(self.batch, device=self.options.get("device"), comm=self.mpicomm,
-                                   node_names=self.node_names)
+                                   node_names=self.node_names, shared=self.options.get("shared_matrix"))
 
     # options the reference's cfg_vanilla.shared_options passes to MIP/LP plugins
     # (threads, mipgap; cfg_vanilla.py:41-62) or that only drive plugin output (Tee):
