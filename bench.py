@@ -9,6 +9,7 @@ iterations are outside it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scens S] [--cm CM]
     python bench.py --model aircond --bf 32,32,64     # config 4 (multistage)
+    python bench.py --model uc [--scens 1000]          # config 5 (UC LP relaxation, path 4)
 
 --gpus N > 1 started without torch.distributed.run launches itself with N local ranks
 (one per GPU, RCCL).  ``--backend gloo`` lets several ranks share one GPU (a functional
@@ -47,12 +48,14 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--scens", type=int, default=65536)
     p.add_argument("--cm", type=int, default=1)
-    p.add_argument("--model", choices=["farmer", "aircond"], default="farmer",
-                   help="farmer (config 3, the headline) or aircond (config 4, multistage)")
+    p.add_argument("--model", choices=["farmer", "aircond", "uc"], default="farmer",
+                   help="farmer (config 3, the headline), aircond (config 4, multistage) or uc "
+                        "(config 5: the UC LP relaxation, 1,000 wind scenarios)")
     p.add_argument("--bf", type=str, default="32,32,64",
                    help="aircond branching factors (scenarios = their product)")
     p.add_argument("--rho", type=float, default=1.0)
-    p.add_argument("--eps", type=float, default=1e-9)
+    p.add_argument("--eps", type=float, default=None,
+                   help="PDHG eps_rel of the PH solves (default 1e-9; uc: 1e-6 for Iter0 and PH)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                    help="torch.distributed backend for N > 1 (auto: RCCL when every rank has its own GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -203,6 +206,8 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
     elif path == 3:
         kname = f"k_solve_wg<{kinfo['wKC']}, {kinfo['wZC']}, {kinfo['wKR']}, {kinfo['wZR']}, {kinfo['wps']}>"
         lanes = 64 * kinfo["wps"]
+    elif path == 4:
+        return roofline_stream(b, launches, ws_bytes, tag, pdir)
     else:
         kname, lanes = "k_solve", 1
     launch_ms = float(np.mean([t for t, _ in launches]))
@@ -238,6 +243,83 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
     return out
 
 
+def roofline_stream(b, launches, ws_bytes, tag, pdir):
+    """Roofline of the shared-matrix streaming kernel (path 4): HBM-bound.
+    Algorithmic bytes per scenario-iteration = 8 (5n + 4m): X, X0 read and X, U written,
+    U read once by the row-pass gathers (n each); Y, Y0 read, Y written and Y read once
+    by the column-pass gathers (m each).  The shared matrix and the shared column / row
+    data are L2 / MALL-resident and not counted.  Measured HBM bytes (PMC) alongside."""
+    n, m, nnz = b.n, b.m, b.nnz
+    kname = "k_solve_stream"
+    launch_ms = float(np.mean([t for t, _ in launches]))
+    units = float(np.mean([u for _, u in launches]))
+    B = 8 * (5 * n + 4 * m)
+    gbs = B * units / (launch_ms * 1e-3) / 1e9
+    traffic, src = None, None
+    pmc = _latest_profile_file(f"pmc_summary_{tag}.json", pdir)
+    if pmc:
+        try:
+            d = json.load(open(pmc))
+            tr = d.get("solve_traffic_bytes_per_launch", {}).get("void " + kname)
+            if tr is not None:
+                traffic = tr["total_upper"]
+                src = os.path.relpath(pmc, ROOT)
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": B * units,
+            "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
+            "kernel": kname, "lanes_per_scenario": 1024, "launch_ms": launch_ms,
+            "scenario_iters_per_launch": units, "bytes_per_scenario_iter": B,
+            "flops_per_scenario_iter": 4 * nnz + 10 * n + 6 * m,
+            "note": ("achieved = 8 (5n + 4m) bytes x scenario-iterations per launch / mean HIP-event launch "
+                     "time; one workgroup streams one scenario's iterates (X X0 U / Y Y0) per PDHG "
+                     "iteration, the shared scaled matrix stays in L2 / MALL")}
+
+
+def uc_cpu_baseline(S_total, sample, rho_vec):
+    """CPU proxy of one PH iteration of config 5 on a bounded sample: per scenario one
+    HiGHS dual-simplex solve (scipy) of the W-augmented LP -- the prox term dropped, since
+    no sparse QP solver is in this image; a QP solve costs at least as much, so this
+    over-states the CPU rate -- with a W from one PH update of the sample, one process
+    per core of the process's CPU share."""
+    import multiprocessing as mp
+    model, ncpu, aff = _host_cpu()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    P = max(1, min(aff, share, sample) if share > 0 else min(aff, sample))
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(P) as pool:
+        res = pool.map(_uc_cpu_worker, [(k, S_total, rho_vec) for k in range(1, sample + 1)])
+    wall = time.perf_counter() - t0
+    per_scen = float(np.median([r for r in res]))
+    t_it = per_scen * S_total / P
+    return {"value": 1.0 / t_it, "unit": "PH iterations/s", "cores": P, "kind": "port",
+            "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "sample": (f"uc: {sample} of {S_total} scenarios, one HiGHS dual-simplex LP each (the W-augmented "
+                       f"PH subproblem without its prox term: no sparse QP solver here, so this is an upper "
+                       f"bound on the CPU rate); median {per_scen:.2f}s per solve, {P} workers -> "
+                       f"{S_total} solves per PH iteration"),
+            "wall_seconds": wall}
+
+
+def _uc_cpu_worker(args):
+    k, S_total, rho_vec = args
+    import warnings
+    warnings.simplefilter("ignore")
+    from mpisppy_amd.examples import uc
+    from oracle import uc as ouc
+    b = uc.batch_creator([f"Scenario{k}"], num_scens=S_total)
+    x, _, _ = ouc.solve_lp(b, 0)
+    on = x[b.nonant_col]
+    W = rho_vec * (on - 0.5)                     # one PH update away from x̄ = 0.5
+    c = b.c[0].copy()
+    c[b.nonant_col] += W
+    t = time.perf_counter()
+    ouc.solve_lp(b, 0, c=c)
+    return time.perf_counter() - t
+
+
 # ---------------------------------------------------------------- GPU run
 def main():
     a = parse()
@@ -251,6 +333,10 @@ def main():
     if a.model == "aircond":
         a.bf = [int(v) for v in a.bf.split(",")]
         a.scens = int(np.prod(a.bf))
+    if a.model == "uc" and a.scens == 65536:
+        a.scens = 1000
+    if a.eps is None:
+        a.eps = 1e-6 if a.model == "uc" else 1e-9
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.model == "farmer":
         sample = a.cpu_sample or min(a.scens, 4096 if a.cm == 1 else 256)
@@ -295,6 +381,21 @@ def main():
         tag = f"farmer{a.scens}_cm{a.cm}"
         workload = {(65536, 1): "farmer PH (config 3)",
                     (1024, 10): "farmer PH (config 2)"}.get((a.scens, a.cm), f"farmer PH, cm={a.cm}")
+    elif a.model == "uc":
+        # config 5: UC LP relaxation (examples/uc.py restating ReferenceModel_OK.py), the
+        # wind scenarios of 1000scenarios_wind; rho = uc_funcs.py:99-116 (0.1 x midpoint cost)
+        from mpisppy_amd.examples import uc
+        names = uc.scenario_names_creator(a.scens)
+        opts["batch_creator"] = uc.batch_creator
+        opts["iter0_solver_options"] = {"eps_rel": a.eps}
+        rho_vec = uc.rho_vector(uc.scenario_creator(names[0], num_scens=a.scens))
+        opts["rho_array"] = rho_vec
+        ph = PH(opts, names, uc.scenario_creator, mpicomm=comm, scenario_creator_kwargs={"num_scens": a.scens})
+        tag = f"uc{a.scens}"
+        workload = "UC LP relaxation PH (config 5)"
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            cpu = uc_cpu_baseline(a.scens, a.cpu_sample or 16, rho_vec)
+            log("cpu baseline:", json.dumps(cpu))
     else:
         # config 4: aircond multistage (aircond.py:37-330), one scenario per leaf of the bf
         # tree; per-node x̄ over all non-leaf nodes
@@ -349,7 +450,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": (f"synthetic ({a.model} scenario generator, seeded as "
+            "data": ("reference data (paperruns/larger_uc RootNode.dat + 1000scenarios_wind/Node*.dat)"
+                     if a.model == "uc" else
+                     f"synthetic ({a.model} scenario generator, seeded as "
                      f"{'farmer.py:52-60' if a.model == 'farmer' else 'aircond.py:37-67'})"),
             "config": {"workload": workload, "scenarios": a.scens,
                        "crops_multiplier": a.cm if a.model == "farmer" else None,

@@ -95,6 +95,13 @@ struct phgpu_state {
     int np, nr;
     int32_t *cmap, *rmap, *pcol, *prow;
     double *sh_col, *sh_row, *sh_norm, *sh_v, *sh_u, *sh_w, *sh_part;
+    // sliced-ELL copies of the scaled matrix for the two streaming passes: slice = 64
+    // consecutive columns (rows), padded to its longest; entry k of slice member l at
+    // off[slice] + 64 k + l (coalesced); *_src = CSC / CSR position of the entry, -1 = pad
+    int nsl_c, nsl_r, nent_c, nent_r;
+    int32_t *cs_off, *cs_len, *cs_idx, *cs_src, *rs_off, *rs_len, *rs_idx, *rs_src;
+    double *cs_val, *rs_val;
+    int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
     double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
     int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
     // PH state (caller-owned)
@@ -1087,6 +1094,71 @@ static hipError_t pack_fill(phgpu_state* h, hipStream_t st) {
     return hipSuccess;
 }
 
+// sliced-ELL layout of the shared pattern (rows and columns in slices of 64); values are
+// filled from the scaled CSR / CSC copies by k_sh_sell_vals
+static int sell_one(phgpu_state* h, int K, const std::vector<int32_t>& ptr, const std::vector<int32_t>& idx,
+                    const std::vector<int32_t>& src, int& nsl, int& nent, int32_t** d_off, int32_t** d_len, int32_t** d_idx,
+                    int32_t** d_src, double** d_val) {
+    nsl = (K + WAVE - 1) / WAVE;
+    std::vector<int32_t> off((size_t)nsl + 1), len((size_t)nsl);
+    int64_t tot = 0;
+    for (int sl = 0; sl < nsl; ++sl) {
+        int L = 0;
+        for (int l = 0; l < WAVE; ++l) {
+            const int r = sl * WAVE + l;
+            if (r < K) L = std::max(L, ptr[r + 1] - ptr[r]);
+        }
+        off[sl] = (int32_t)tot;
+        len[sl] = L;
+        tot += (int64_t)L * WAVE;
+        if (tot >= (1LL << 31)) return set_err(-1, "sliced-ELL copy too large");
+    }
+    off[nsl] = (int32_t)tot;
+    nent = (int)tot;
+    std::vector<int32_t> e_idx((size_t)std::max<int64_t>(tot, 1), 0), e_src((size_t)std::max<int64_t>(tot, 1), -1);
+    for (int sl = 0; sl < nsl; ++sl)
+        for (int l = 0; l < WAVE; ++l) {
+            const int r = sl * WAVE + l;
+            if (r >= K) continue;
+            for (int k = 0; k < ptr[r + 1] - ptr[r]; ++k) {
+                const size_t e = (size_t)off[sl] + (size_t)k * WAVE + l;
+                e_idx[e] = idx[ptr[r] + k];
+                e_src[e] = src[ptr[r] + k];
+            }
+        }
+    if (dalloc(h, d_off, off.size()) || dalloc(h, d_len, len.size()) || dalloc(h, d_idx, e_idx.size()) ||
+        dalloc(h, d_src, e_src.size()) || dalloc(h, d_val, e_idx.size()))
+        return -3;
+    hipError_t e = hipMemcpy(*d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(*d_len, len.data(), std::max<size_t>(len.size(), 1) * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(*d_idx, e_idx.data(), e_idx.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(*d_src, e_src.data(), e_src.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return set_err(-2, "sliced-ELL upload failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+static int build_sell(phgpu_state* h, const int32_t* row_ptr, const int32_t* col_idx) {
+    const int n = h->n, m = h->m, nnz = h->nnz;
+    // rows: CSR as given, source = CSR position
+    std::vector<int32_t> rp(row_ptr, row_ptr + m + 1), ci(col_idx, col_idx + nnz), rsrc((size_t)nnz);
+    for (int k = 0; k < nnz; ++k) rsrc[k] = k;
+    int rc = sell_one(h, m, rp, ci, rsrc, h->nsl_r, h->nent_r, &h->rs_off, &h->rs_len, &h->rs_idx, &h->rs_src, &h->rs_val);
+    if (rc) return rc;
+    // columns: the CSC order of phgpu_create (rows ascending within a column), source =
+    // CSC position
+    std::vector<int32_t> cp((size_t)n + 1, 0), ri((size_t)nnz), csrc((size_t)nnz);
+    for (int k = 0; k < nnz; ++k) cp[col_idx[k] + 1]++;
+    for (int j = 0; j < n; ++j) cp[j + 1] += cp[j];
+    std::vector<int32_t> fill(cp.begin(), cp.end() - 1);
+    for (int i = 0; i < m; ++i)
+        for (int k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+            const int p = fill[col_idx[k]]++;
+            ri[p] = i;
+            csrc[p] = p;
+        }
+    return sell_one(h, n, cp, ri, csrc, h->nsl_c, h->nent_c, &h->cs_off, &h->cs_len, &h->cs_idx, &h->cs_src, &h->cs_val);
+}
+
 extern "C" int phgpu_default_options(phgpu_options* o) {
     if (!o) return set_err(-1, "null options");
     o->eps_rel = 1e-9;
@@ -1219,6 +1291,8 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         ALLOC(h->sh_u, n);
         ALLOC(h->sh_w, m);
         ALLOC(h->sh_part, (size_t)(n + 255) / 256 + 1);
+        ALLOC(h->sk_iters, Sz);
+        ALLOC(h->sk_order, Sz);
     } else {
         ALLOC(h->A, (size_t)nnz * Sz);
         ALLOC(h->c, (size_t)n * Sz);
@@ -1290,6 +1364,11 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     h->reg_inst = -1;
     h->wg_inst = -1;
     if (h->shared) {
+        const int rcs = build_sell(h, row_ptr, col_idx);
+        if (rcs) {
+            phgpu_destroy(h);
+            return rcs;
+        }
         h->default_kernel = 4;
         *out = h;
         return 0;
@@ -1444,6 +1523,13 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
         hipLaunchKernelGGL(k_sh_apply, gb, dim3(256), 0, st, *h, (const double*)h->sh_w, (const double*)h->sh_u);
     }
     hipLaunchKernelGGL(k_sh_csc, gz, dim3(256), 0, st, *h);
+    {
+        const int tot_c = h->nent_c, tot_r = h->nent_r;
+        if (tot_c) hipLaunchKernelGGL(k_sh_sell_vals, dim3((unsigned)((tot_c + 255) / 256)), dim3(256), 0, st,
+                                      (const int32_t*)h->cs_src, (const double*)h->Ah_csc, tot_c, h->cs_val);
+        if (tot_r) hipLaunchKernelGGL(k_sh_sell_vals, dim3((unsigned)((tot_r + 255) / 256)), dim3(256), 0, st,
+                                      (const int32_t*)h->rs_src, (const double*)h->Ah_csr, tot_r, h->rs_val);
+    }
     // ||A_scaled||_2: 200 power iterations on A^T A
     hipLaunchKernelGGL(k_sh_vinit, gn, dim3(256), 0, st, *h, h->sh_v);
     for (int it = 0; it < 200; ++it) {
@@ -1624,6 +1710,13 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > h->S) nblk = h->S;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
+        // queue order: longest first by the previous solve's iteration counts (the launch
+        // ends with its slowest scenario; starting it first shortens the tail)
+        if (!h->have_solution) HIPCHK(hipMemsetAsync(h->sk_iters, 0, (size_t)h->S * sizeof(int32_t), st));
+        if (h->S <= STREAM_ORDER_MAX)
+            hipLaunchKernelGGL(k_stream_order, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
+        else
+            hipLaunchKernelGGL(k_stream_order_identity, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
         hipLaunchKernelGGL(k_solve_stream, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj, bound,
                            status, iters);
         HIPCHK(hipGetLastError());
@@ -1795,7 +1888,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->pl_col_r, h->pl_row_k, h->pl_row_c, h->qhead, h->wg_col_id, h->wg_row_id,
                     h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c,
                     h->pk, h->cmap, h->rmap, h->pcol, h->prow, h->sh_col, h->sh_row, h->sh_norm, h->sh_v,
-                    h->sh_u, h->sh_w, h->sh_part, h->sk};
+                    h->sh_u, h->sh_w, h->sh_part, h->sk, h->cs_off, h->cs_len, h->cs_idx, h->cs_src,
+                    h->rs_off, h->rs_len, h->rs_idx, h->rs_src, h->cs_val, h->rs_val, h->sk_iters, h->sk_order};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;

@@ -162,9 +162,14 @@ class PHEngine:
 
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):
-        """rho: scalar or host [S, nn] array (the rho Params of phbase.py:598-602)."""
+        """rho: scalar, host [nn] array (the same per-nonant rho in every scenario) or host
+        [S, nn] array (the rho Params of phbase.py:598-602)."""
         if np.isscalar(rho):
             self.rho.fill_(float(rho))
+        elif np.ndim(rho) == 1:
+            r = torch.as_tensor(np.asarray(rho, dtype=np.float64), device=self.device)
+            assert r.shape[0] == self.nn, (r.shape, self.nn)
+            self.rho[:self.nn].copy_(r[:, None].expand(self.nn, self.S))
         else:
             self.rho.copy_(_dev_T(np.asarray(rho, dtype=np.float64), self.device))
 

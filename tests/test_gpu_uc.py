@@ -1,0 +1,166 @@
+"""The shared-matrix streaming path (path 4, include/phgpu.h PHGPU_SHARED_MATRIX) on the
+GPU: config 5 (UC LP relaxation) against HiGHS (tests/golden/uc.json -- parity UNPINNED,
+see make_golden_uc.py), and path 4 against the other paths and the oracle on models
+whose matrix is the same in every scenario (aircond, the tiny infeasibility batch)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "uc.json")))
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+UC_EPS = 1e-6          # the tolerance config 5 runs at (bench.py --model uc)
+UC_OBJ_REL = 1e-5
+
+
+def test_uc_lp_relaxation_vs_highs(gpu):
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import uc
+    names = GOLD["names"]
+    b = uc.batch_creator(names, num_scens=GOLD["num_scens"])
+    e = PHEngine(b, device="cuda:0")
+    info = e.kernel_info()
+    assert e.shared and info["path"] == 4, info
+    e.solve(_lib.default_options(eps_rel=UC_EPS), warm=False)
+    st, obj, bnd = e.host("status"), e.host("obj"), e.host("bound")
+    assert (st == _lib.OPTIMAL).all(), (st, e.host("iters"))
+    want = np.array(GOLD["lp_obj"])
+    assert np.all(np.abs(obj - want) <= UC_OBJ_REL * np.abs(want)), (obj, want)
+    assert np.all(np.abs(bnd - want) <= UC_OBJ_REL * np.abs(want)), (bnd, want)
+    # the returned x is (nearly) feasible in the original units
+    x = e.host("x")
+    for s in range(2):
+        A = b.dense_A(s) if b.n * b.m < 1e8 else None
+        if A is None:
+            from oracle import uc as ouc
+            ax = ouc.scenario_matrix(b, s) @ x[s]
+        else:
+            ax = A @ x[s]
+        scale = 1 + np.abs(np.where(np.isfinite(b.rl[s]), b.rl[s], 0)) + \
+            np.abs(np.where(np.isfinite(b.ru[s]), b.ru[s], 0))
+        viol = np.maximum(b.rl[s] - ax, 0) + np.maximum(ax - b.ru[s], 0)
+        assert np.linalg.norm(viol) <= 1e-4 * np.linalg.norm(scale)
+        assert np.all(x[s] >= b.lb[s] - 1e-7) and np.all(x[s] <= b.ub[s] + 1e-7)
+    # warm start: the same answer, fewer iterations
+    it0 = e.host("iters").copy()
+    e.solve(_lib.default_options(eps_rel=UC_EPS), warm=True)
+    assert np.all(np.abs(e.host("obj") - want) <= UC_OBJ_REL * np.abs(want))
+    assert e.host("iters").max() < it0.max()
+    e.close()
+
+
+def test_uc_ph_iterations(gpu):
+    """Three PH iterations of config 5 on 8 scenarios (uc_funcs.py rho setter): every
+    subproblem solved, W moves, the PH objective terms reach the kernel."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import uc
+    names = GOLD["names"]
+    rho = uc.rho_vector(uc.scenario_creator(names[0], num_scens=GOLD["num_scens"]))
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 3, "defaultPHrho": 1.0, "convthresh": -1.0,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": uc.batch_creator, "rho_array": rho,
+            "iter0_solver_options": {"eps_rel": UC_EPS}, "iterk_solver_options": {"eps_rel": UC_EPS}}
+    ph = PH(opts, names, uc.scenario_creator, scenario_creator_kwargs={"num_scens": len(names)})
+    conv, eobj, tb = ph.ph_main()
+    e = ph.engine
+    assert e.kernel_info()["path"] == 4
+    assert e.count_not_optimal() == 0
+    # trivial bound = probability-weighted Iter0 LP bounds (8 scenarios, p = 1/8)
+    want = np.mean(GOLD["lp_obj"])
+    assert abs(tb - want) <= UC_OBJ_REL * abs(want), (tb, want)
+    W = ph.W_array()
+    assert np.abs(W).max() > 0 and np.isfinite(conv)
+    # sum_s p_s W_s = 0 at every nonant (PH keeps the probability-weighted W at zero)
+    assert np.abs(W.sum(axis=0)).max() <= 1e-6 * max(1.0, np.abs(W).max())
+
+
+def test_path4_matches_default_path_on_aircond(gpu):
+    """aircond has the same matrix in every scenario: solve it on path 4 and on the
+    default path; then 5 PH iterations on path 4 against the oracle's W trajectory."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import aircond
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+    g = GOLDEN["aircond432_rho1"]
+    kw = dict(g["kwargs"])
+    kw["branching_factors"] = g["branching_factors"]
+    names = g["names"]
+    b = aircond.batch_creator(names, **kw)
+    e2 = PHEngine(b, device="cuda:0", shared=False)
+    e4 = PHEngine(b, device="cuda:0", shared=True)
+    assert e4.kernel_info()["path"] == 4 and e2.kernel_info()["path"] != 4
+    for e in (e2, e4):
+        e.solve(_lib.default_options(), warm=False)
+    assert (e4.host("status") == 0).all()
+    o2, o4 = e2.host("obj"), e4.host("obj")
+    assert np.all(np.abs(o2 - o4) <= 1e-7 * np.maximum(1.0, np.abs(o2)))
+    assert np.abs(e2.host("x") - e4.host("x")).max() <= 1e-5
+    with pytest.raises(_lib.PhgpuError, match="path 4 only"):
+        e4.solve(_lib.default_options(kernel=2), warm=False)
+    with pytest.raises(_lib.PhgpuError, match="path 4 only"):
+        e2.solve(_lib.default_options(kernel=4), warm=False)
+    e2.close()
+    e4.close()
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": 1e-10,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "shared_matrix": True, "batch_creator": aircond.batch_creator}
+    ph = PH(opts, names, aircond.scenario_creator, scenario_creator_kwargs=kw,
+            all_nodenames=create_nodenames_from_branching_factors(g["branching_factors"]))
+    conv, eobj, tb = ph.ph_main()
+    assert ph.engine.kernel_info()["path"] == 4
+    assert abs(tb - g["trivial_bound"]) <= 1e-5 * abs(g["trivial_bound"])
+    assert np.abs(ph.W_array() - np.array(g["traj5"][4]["W"])).max() <= 1e-5
+
+
+@pytest.mark.parametrize("kind,code", [("primal", 2), ("dual", 3)])
+def test_path4_certifies_infeasibility(gpu, kind, code):
+    """The tiny batch of test_gpu_scale.py (one matrix for all scenarios): the bad
+    scenario's row range (primal) / cost (dual) is per-scenario data on path 4."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from test_gpu_scale import _tiny_batch
+    S, bad = 70, 37
+    e = PHEngine(_tiny_batch(S, bad, kind), device="cuda:0", shared=True)
+    assert e.kernel_info()["path"] == 4
+    e.solve(_lib.default_options(), warm=False)
+    st, it, obj = e.host("status"), e.host("iters"), e.host("obj")
+    assert st[bad] == code and it[bad] <= 4096, (st[bad], it[bad])
+    others = np.delete(np.arange(S), bad)
+    assert (st[others] == _lib.OPTIMAL).all()
+    assert np.isinf(obj[bad]) and (obj[bad] > 0) == (code == 2)
+    assert np.abs(obj[others] + 8.0).max() <= 1e-6
+    e.close()
+
+
+def test_path4_fix_nonants(gpu):
+    """phgpu_fix_nonants on a shared-matrix handle (the xhat evaluation of the
+    spokes): fixing every nonant at a feasible point's values reproduces its objective
+    through the per-scenario bound records; NULL restores the model bounds."""
+    import torch
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import aircond
+    g = GOLDEN["aircond432_rho1"]
+    kw = dict(g["kwargs"])
+    kw["branching_factors"] = g["branching_factors"]
+    b = aircond.batch_creator(g["names"], **kw)
+    e = PHEngine(b, device="cuda:0", shared=True)
+    e.solve(_lib.default_options(), warm=False)
+    o_free = e.host("obj").copy()
+    xfix = e.nonant_x_dev().clone()
+    e.fix_nonants(0.5 * xfix)                      # another (feasible: overtime covers) first stage
+    e.solve(_lib.default_options(), warm=True)
+    assert (e.host("status") == 0).all()
+    xn = e.nonant_x_dev()
+    assert torch.allclose(xn, 0.5 * xfix, atol=1e-9)
+    assert np.all(e.host("obj") >= o_free - 1e-7 * np.abs(o_free))
+    e.fix_nonants(None)
+    e.solve(_lib.default_options(), warm=True)
+    assert np.all(np.abs(e.host("obj") - o_free) <= 1e-7 * np.maximum(1.0, np.abs(o_free)))
+    e.close()
