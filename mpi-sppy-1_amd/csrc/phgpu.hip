@@ -101,6 +101,9 @@ struct phgpu_state {
     int nsl_c, nsl_r, nent_c, nent_r;
     int32_t *cs_off, *cs_len, *cs_idx, *cs_src, *rs_off, *rs_len, *rs_idx, *rs_src;
     double *cs_val, *rs_val;
+    // slices of each pass per wave of the streaming workgroup (balanced by entries):
+    // wave w takes cw_slc[cw_ptr[w] .. cw_ptr[w+1]) (rw_* for rows)
+    int32_t *cw_ptr, *cw_slc, *rw_ptr, *rw_slc;
     int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
     double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
     int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
@@ -1098,7 +1101,7 @@ static hipError_t pack_fill(phgpu_state* h, hipStream_t st) {
 // filled from the scaled CSR / CSC copies by k_sh_sell_vals
 static int sell_one(phgpu_state* h, int K, const std::vector<int32_t>& ptr, const std::vector<int32_t>& idx,
                     const std::vector<int32_t>& src, int& nsl, int& nent, int32_t** d_off, int32_t** d_len, int32_t** d_idx,
-                    int32_t** d_src, double** d_val) {
+                    int32_t** d_src, double** d_val, int32_t** d_wptr, int32_t** d_wslc) {
     nsl = (K + WAVE - 1) / WAVE;
     std::vector<int32_t> off((size_t)nsl + 1), len((size_t)nsl);
     int64_t tot = 0;
@@ -1126,13 +1129,36 @@ static int sell_one(phgpu_state* h, int K, const std::vector<int32_t>& ptr, cons
                 e_src[e] = src[ptr[r] + k];
             }
         }
+    // slices -> waves of the streaming workgroup: longest first onto the least loaded wave
+    // (cost = entries per lane + a fixed per-slice overhead), each wave's list in slice order
+    std::vector<int32_t> bysz((size_t)nsl);
+    for (int sl = 0; sl < nsl; ++sl) bysz[sl] = sl;
+    std::stable_sort(bysz.begin(), bysz.end(), [&](int a, int b) { return len[a] > len[b]; });
+    std::vector<int64_t> load(SWAVES, 0);
+    std::vector<std::vector<int32_t>> lists(SWAVES);
+    for (int sl : bysz) {
+        int w = 0;
+        for (int v = 1; v < SWAVES; ++v)
+            if (load[v] < load[w]) w = v;
+        load[w] += len[sl] + 4;
+        lists[w].push_back(sl);
+    }
+    std::vector<int32_t> wptr(SWAVES + 1, 0), wslc;
+    for (int w = 0; w < SWAVES; ++w) {
+        std::sort(lists[w].begin(), lists[w].end());
+        wslc.insert(wslc.end(), lists[w].begin(), lists[w].end());
+        wptr[w + 1] = (int32_t)wslc.size();
+    }
     if (dalloc(h, d_off, off.size()) || dalloc(h, d_len, len.size()) || dalloc(h, d_idx, e_idx.size()) ||
-        dalloc(h, d_src, e_src.size()) || dalloc(h, d_val, e_idx.size()))
+        dalloc(h, d_src, e_src.size()) || dalloc(h, d_val, e_idx.size()) || dalloc(h, d_wptr, wptr.size()) ||
+        dalloc(h, d_wslc, std::max<size_t>(wslc.size(), 1)))
         return -3;
     hipError_t e = hipMemcpy(*d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(*d_len, len.data(), std::max<size_t>(len.size(), 1) * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(*d_idx, e_idx.data(), e_idx.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(*d_src, e_src.data(), e_src.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(*d_wptr, wptr.data(), wptr.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !wslc.empty()) e = hipMemcpy(*d_wslc, wslc.data(), wslc.size() * 4, hipMemcpyHostToDevice);
     if (e != hipSuccess) return set_err(-2, "sliced-ELL upload failed: %s", hipGetErrorString(e));
     return 0;
 }
@@ -1142,7 +1168,8 @@ static int build_sell(phgpu_state* h, const int32_t* row_ptr, const int32_t* col
     // rows: CSR as given, source = CSR position
     std::vector<int32_t> rp(row_ptr, row_ptr + m + 1), ci(col_idx, col_idx + nnz), rsrc((size_t)nnz);
     for (int k = 0; k < nnz; ++k) rsrc[k] = k;
-    int rc = sell_one(h, m, rp, ci, rsrc, h->nsl_r, h->nent_r, &h->rs_off, &h->rs_len, &h->rs_idx, &h->rs_src, &h->rs_val);
+    int rc = sell_one(h, m, rp, ci, rsrc, h->nsl_r, h->nent_r, &h->rs_off, &h->rs_len, &h->rs_idx, &h->rs_src, &h->rs_val,
+                      &h->rw_ptr, &h->rw_slc);
     if (rc) return rc;
     // columns: the CSC order of phgpu_create (rows ascending within a column), source =
     // CSC position
@@ -1156,7 +1183,8 @@ static int build_sell(phgpu_state* h, const int32_t* row_ptr, const int32_t* col
             ri[p] = i;
             csrc[p] = p;
         }
-    return sell_one(h, n, cp, ri, csrc, h->nsl_c, h->nent_c, &h->cs_off, &h->cs_len, &h->cs_idx, &h->cs_src, &h->cs_val);
+    return sell_one(h, n, cp, ri, csrc, h->nsl_c, h->nent_c, &h->cs_off, &h->cs_len, &h->cs_idx, &h->cs_src, &h->cs_val,
+                    &h->cw_ptr, &h->cw_slc);
 }
 
 extern "C" int phgpu_default_options(phgpu_options* o) {
@@ -1889,7 +1917,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->wg_col_long, h->wg_row_long, h->wg_col_k, h->wg_col_r, h->wg_row_k, h->wg_row_c,
                     h->pk, h->cmap, h->rmap, h->pcol, h->prow, h->sh_col, h->sh_row, h->sh_norm, h->sh_v,
                     h->sh_u, h->sh_w, h->sh_part, h->sk, h->cs_off, h->cs_len, h->cs_idx, h->cs_src,
-                    h->rs_off, h->rs_len, h->rs_idx, h->rs_src, h->cs_val, h->rs_val, h->sk_iters, h->sk_order};
+                    h->rs_off, h->rs_len, h->rs_idx, h->rs_src, h->cs_val, h->rs_val, h->sk_iters, h->sk_order,
+                    h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;

@@ -13,5 +13,5 @@ step() {
 for S in 1 16 64 256 512 1000; do step ucprof_S$S 300 python -u tools/uc_prof.py $S 2048; done
 step pmc_fetch_uc 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_uc -o run -- python3 tools/uc_prof.py 512 2048
 step pmc_write_uc 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_uc -o run -- python3 tools/uc_prof.py 512 2048
-step pmc_sq_uc 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/pmc_sq_uc -o run -- python3 tools/uc_prof.py 512 2048
+step pmc_sq_uc 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc_sq_uc -o run -- python3 tools/uc_prof.py 512 2048
 echo done
