@@ -1733,10 +1733,14 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     if (h->shared) {
         if (!h->scen_set) return set_err(-1, "phgpu_set_scenarios has not been called");
         int per_cu = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_solve_stream, SBLK, 0));
+        // B scenario slots per workgroup (PHGPU_STREAM_SLOTS=1|2, default 2)
+        const char* env = getenv("PHGPU_STREAM_SLOTS");
+        const int B = (env && atoi(env) == 1) ? 1 : 2;
+        const void* fn = B == 1 ? (const void*)k_solve_stream<1> : (const void*)k_solve_stream<2>;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, SBLK, 0));
         if (per_cu < 1) per_cu = 1;
         int64_t nblk = (int64_t)per_cu * h->num_cus;
-        if (nblk > h->S) nblk = h->S;
+        if (nblk > (h->S + B - 1) / B) nblk = (h->S + B - 1) / B;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
         // queue order: longest first by the previous solve's iteration counts (the launch
         // ends with its slowest scenario; starting it first shortens the tail)
@@ -1745,8 +1749,12 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             hipLaunchKernelGGL(k_stream_order, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
         else
             hipLaunchKernelGGL(k_stream_order_identity, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
-        hipLaunchKernelGGL(k_solve_stream, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj, bound,
-                           status, iters);
+        if (B == 1)
+            hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+                               bound, status, iters);
+        else
+            hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+                               bound, status, iters);
         HIPCHK(hipGetLastError());
         h->have_solution = 1;
         h->last_path = 4;
