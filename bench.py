@@ -250,7 +250,8 @@ def roofline_stream(b, launches, ws_bytes, tag, pdir):
     by the column-pass gathers (m each).  The shared matrix and the shared column / row
     data are L2 / MALL-resident and not counted.  Measured HBM bytes (PMC) alongside."""
     n, m, nnz = b.n, b.m, b.nnz
-    kname = "k_solve_stream"
+    slots = 1 if os.environ.get("PHGPU_STREAM_SLOTS") == "1" else 2      # phgpu_solve's choice
+    kname = f"k_solve_stream<{slots}>"
     launch_ms = float(np.mean([t for t, _ in launches]))
     units = float(np.mean([u for _, u in launches]))
     B = 8 * (5 * n + 4 * m)
@@ -260,16 +261,15 @@ def roofline_stream(b, launches, ws_bytes, tag, pdir):
     if pmc:
         try:
             d = json.load(open(pmc))
-            tr = d.get("solve_traffic_bytes_per_launch", {}).get("void " + kname)
-            if tr is not None:
-                traffic = tr["total_upper"]
+            if d.get("kernel") == "void " + kname:
+                traffic = d["bytes_per_scenario_iter"]["total_upper"] * units
                 src = os.path.relpath(pmc, ROOT)
         except Exception:
             traffic = None
     return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": B * units,
             "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
-            "kernel": kname, "lanes_per_scenario": 1024, "launch_ms": launch_ms,
+            "kernel": kname, "lanes_per_scenario": 1024 // slots, "launch_ms": launch_ms,
             "scenario_iters_per_launch": units, "bytes_per_scenario_iter": B,
             "flops_per_scenario_iter": 4 * nnz + 10 * n + 6 * m,
             "note": ("achieved = 8 (5n + 4m) bytes x scenario-iterations per launch / mean HIP-event launch "
