@@ -15,11 +15,11 @@ order (uc_funcs.py:78-83 -> sputils.attach_root_node -> scenario_tree.py:39); th
 probability is uniform (ScenarioStructure.dat: 0.001 each for 1000 scenarios).
 
 ``path`` (the reference's kwarg) names a directory holding ``RootNode.dat`` and
-``NodeN.dat``; without it the packaged copy of the 1000-scenario data is used
-(``uc_data/``: RootNode.dat plus the wind bounds of Node1..1000.dat, packed by
-tools/make_uc_data.py).
+``NodeN.dat``; without it the packaged form of the 1000-scenario data is used
+(``uc_data/``: RootNode.dat's parsed parameters and sets, and the wind bounds of
+Node1..1000.dat, packed by tools/make_uc_data.py).
 """
-import math
+import json
 import os
 
 import numpy as np
@@ -27,7 +27,7 @@ import numpy as np
 from ..model import LinearModel, INF
 from ..sputils import extract_num, attach_root_node
 from ..batch import ScenarioBatch, batch_from_models
-from ..utils.datfile import load_dat
+from ..utils.datfile import load_dat, load_data
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "uc_data")
 BIG_PENALTY = 1e6              # ReferenceModel_OK.py:995-999
@@ -40,9 +40,13 @@ _ROOT_CACHE = {}
 
 
 def _root_data(path):
-    key = os.path.abspath(path or DATA_DIR)
+    key = os.path.abspath(path) if path else None
     if key not in _ROOT_CACHE:
-        _ROOT_CACHE[key] = load_dat(os.path.join(key, "RootNode.dat"))
+        if key is None:
+            with open(os.path.join(DATA_DIR, "rootnode.json")) as f:
+                _ROOT_CACHE[key] = load_data(json.load(f))
+        else:
+            _ROOT_CACHE[key] = load_dat(os.path.join(key, "RootNode.dat"))
     p, s = _ROOT_CACHE[key]
     return dict(p), dict(s)
 

@@ -88,3 +88,26 @@ def parse_dat(text, params=None, sets=None):
 def load_dat(path, params=None, sets=None):
     with open(path) as f:
         return parse_dat(f.read(), params, sets)
+
+
+def dump_data(params, sets):
+    """JSON-able form of (params, sets): indexed params as [[key, value], ...] with tuple
+    keys as lists (load_data inverts it exactly)."""
+    P = {}
+    for k, v in params.items():
+        if isinstance(v, dict):
+            P[k] = {"indexed": [[list(kk) if isinstance(kk, tuple) else kk, vv] for kk, vv in v.items()]}
+        else:
+            P[k] = {"scalar": v}
+    return {"params": P, "sets": sets}
+
+
+def load_data(obj):
+    """Inverse of dump_data."""
+    params = {}
+    for k, v in obj["params"].items():
+        if "scalar" in v:
+            params[k] = v["scalar"]
+        else:
+            params[k] = {(tuple(kk) if isinstance(kk, list) else kk): vv for kk, vv in v["indexed"]}
+    return params, {k: list(v) for k, v in obj["sets"].items()}

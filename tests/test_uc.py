@@ -45,6 +45,12 @@ def test_root_node_data():
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference data not present")
+def test_packed_root_data_matches_root_node_file():
+    from mpisppy_amd.examples import uc
+    assert uc._root_data(None) == uc._root_data(REF)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference data not present")
 def test_packed_wind_matches_node_files():
     from mpisppy_amd.examples import uc
     for k in (1, 17, 500, 1000):

@@ -1,21 +1,21 @@
 """Pack the reference's UC data for the GPU box (where /root/reference does not exist).
 
-Copies paperruns/larger_uc/RootNode.dat (data, 40 KB) and packs the wind bounds of
+Parses paperruns/larger_uc/RootNode.dat with the model's own reader and stores the
+parsed parameters and sets as uc_data/rootnode.json, and packs the wind bounds of
 paperruns/larger_uc/1000scenarios_wind/Node1..1000.dat -- the only scenario data --
-into mpisppy_amd/examples/uc_data/wind_1000scen.npz (lo/hi [node, gen, t]).  The
-floats are parsed by the same reader the model uses, so the packed values equal what
-reading the .dat files gives (tests/test_uc.py checks a sample against the files when
+into uc_data/wind_1000scen.npz (lo/hi [node, gen, t]).  Both hold exactly what reading
+the .dat files gives (tests/test_uc.py compares them with the files when
 /root/reference is present).
 """
+import json
 import os
-import shutil
 import sys
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpi-sppy-1_amd"))
-from mpisppy_amd.utils.datfile import load_dat  # noqa: E402
+from mpisppy_amd.utils.datfile import load_dat, dump_data  # noqa: E402
 
 SRC = "/root/reference/paperruns/larger_uc"
 DST = os.path.join(ROOT, "mpi-sppy-1_amd", "mpisppy_amd", "examples", "uc_data")
@@ -23,7 +23,9 @@ DST = os.path.join(ROOT, "mpi-sppy-1_amd", "mpisppy_amd", "examples", "uc_data")
 
 def main():
     os.makedirs(DST, exist_ok=True)
-    shutil.copyfile(os.path.join(SRC, "RootNode.dat"), os.path.join(DST, "RootNode.dat"))
+    p, s = load_dat(os.path.join(SRC, "RootNode.dat"))
+    with open(os.path.join(DST, "rootnode.json"), "w") as f:
+        json.dump(dump_data(p, s), f, separators=(",", ":"))
     wdir = os.path.join(SRC, "1000scenarios_wind")
     nodes = sorted(int(f[4:-4]) for f in os.listdir(wdir) if f.startswith("Node") and f.endswith(".dat"))
     p0, s0 = load_dat(os.path.join(SRC, "RootNode.dat"))
