@@ -27,7 +27,7 @@ import numpy as np
 from ..model import LinearModel, INF
 from ..sputils import extract_num, attach_root_node
 from ..batch import ScenarioBatch, batch_from_models
-from ..utils.datfile import load_dat, load_data
+from ..utils.datfile import load_dat, load_data as load_packed
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "uc_data")
 BIG_PENALTY = 1e6              # ReferenceModel_OK.py:995-999
@@ -44,7 +44,7 @@ def _root_data(path):
     if key not in _ROOT_CACHE:
         if key is None:
             with open(os.path.join(DATA_DIR, "rootnode.json")) as f:
-                _ROOT_CACHE[key] = load_data(json.load(f))
+                _ROOT_CACHE[key] = load_packed(json.load(f))
         else:
             _ROOT_CACHE[key] = load_dat(os.path.join(key, "RootNode.dat"))
     p, s = _ROOT_CACHE[key]
