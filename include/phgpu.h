@@ -185,6 +185,12 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
 int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
                        const int32_t* status, double* out, void* stream);
 
+/* counts[c] = number of local scenarios whose status[s] == c, c = 0..3 (OPTIMAL,
+ * ITER_LIMIT, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE): the check behind SPOpt.solve_loop's
+ * gripe (spopt.py:284-294) as one device reduction.  status: device [S] (phgpu_solve's
+ * output), counts: device int32[4]. */
+int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_t* counts, void* stream);
+
 /* Fix the nonants of every local scenario (lb = ub = xfix[k*S + s], original units,
  * clipped to the model bounds) for the following solves, or restore the model bounds
  * when xfix is NULL.  A NaN entry leaves that nonant at its model bounds (partial

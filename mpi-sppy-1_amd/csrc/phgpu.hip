@@ -89,6 +89,7 @@ struct phgpu_state {
     int scen_set;
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
+    int occ_cache[8];  // workgroups per CU of each solve kernel (0 = not queried yet)
     // shared-matrix handle (PHGPU_SHARED_MATRIX, path 4: solve_stream.inc): one scaled A
     // (A / Ah_csr / Ah_csc [nnz], Dr [m], Dc [n]) for all scenarios; the shared base of
     // the column / row data (sh_col: ch qh lbh ubh, sh_row: rlh ruh rl ru, scenario 0);
@@ -1904,7 +1905,9 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         const char* env = getenv("PHGPU_STREAM_SLOTS");
         const int B = (env && atoi(env) == 1) ? 1 : 2;
         const void* fn = B == 1 ? (const void*)k_solve_stream<1> : (const void*)k_solve_stream<2>;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, SBLK, 0));
+        int& oc = h->occ_cache[B == 1 ? 4 : 5];
+        if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, SBLK, 0));
+        per_cu = oc;
         if (per_cu < 1) per_cu = 1;
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > (h->S + B - 1) / B) nblk = (h->S + B - 1) / B;
@@ -1973,7 +1976,9 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_c = h->wg_row_c;
         const size_t lds = wg_lds_doubles(h->n, h->m, gi.KC, gi.KR, gi.WPS) * sizeof(double);
         int per_cu = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gi.fn, pl.L, lds));
+        int& oc = h->occ_cache[3];
+        if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, (const void*)gi.fn, pl.L, lds));
+        per_cu = oc;
         if (per_cu < 1) per_cu = 1;
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > h->S) nblk = h->S;
@@ -2002,7 +2007,9 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         // persistent grid: co-resident workgroups of REG_WPB independent waves (occupancy
         // x CUs), never more than there are scenario groups
         int per_cu = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, WAVE * REG_WPB, lds));
+        int& oc = h->occ_cache[2];
+        if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, (const void*)fn, WAVE * REG_WPB, lds));
+        per_cu = oc;
         if (per_cu < 1) per_cu = 1;
         const int64_t need = (h->S + (int64_t)G * REG_WPB - 1) / ((int64_t)G * REG_WPB);
         int64_t nblk = (int64_t)per_cu * h->num_cus;
@@ -2057,6 +2064,30 @@ extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const doubl
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_sum_partials, dim3(5), dim3(256), 0, st, (const double*)h->part, h->nwaves, 5, 1.0,
                        out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// counts[c] = number of local scenarios with status c (c = 0..3), one block
+__global__ void __launch_bounds__(1024) k_status_counts(const int32_t* __restrict__ status, int64_t S,
+                                                        int32_t* __restrict__ counts) {
+    __shared__ int32_t c[4];
+    if (threadIdx.x < 4) c[threadIdx.x] = 0;
+    __syncthreads();
+    int32_t loc[4] = {0, 0, 0, 0};
+    for (int64_t s = threadIdx.x; s < S; s += 1024) {
+        const int32_t v = status[s];
+        if (v >= 0 && v < 4) ++loc[v];
+    }
+    for (int k = 0; k < 4; ++k)
+        if (loc[k]) atomicAdd(&c[k], loc[k]);
+    __syncthreads();
+    if (threadIdx.x < 4) counts[threadIdx.x] = c[threadIdx.x];
+}
+
+extern "C" int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_t* counts, void* stream) {
+    if (!h || !status || !counts) return set_err(-1, "null argument");
+    hipLaunchKernelGGL(k_status_counts, dim3(1), dim3(1024), 0, (hipStream_t)stream, status, h->S, counts);
     HIPCHK(hipGetLastError());
     return 0;
 }

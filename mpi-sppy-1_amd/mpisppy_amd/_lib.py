@@ -45,7 +45,7 @@ SHARED_MATRIX = 1          # phgpu_create2 flag (include/phgpu.h)
 # every symbol include/phgpu.h declares (tests check the library exports them all)
 EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_scenarios", "phgpu_set_ph_state",
            "phgpu_solve", "phgpu_ph_reduce", "phgpu_ph_update", "phgpu_expectations",
-           "phgpu_fix_nonants", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
+           "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info"]
 
 _lib = None
@@ -77,6 +77,7 @@ def load(path=None):
     lib.phgpu_ph_update.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]
     lib.phgpu_expectations.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]
     lib.phgpu_fix_nonants.argtypes = [c_vp, c_vp, c_vp]
+    lib.phgpu_status_counts.argtypes = [c_vp, c_vp, c_vp, c_vp]
     lib.phgpu_destroy.argtypes = [c_vp]
     lib.phgpu_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     lib.phgpu_workspace_bytes.argtypes = [c_vp]

@@ -204,26 +204,68 @@ class PHEngine:
         return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
 
     # -------------------------------------------------------------- hot path
-    def solve(self, options=None, warm=True):
+    _OUTS = ("x", "y", "obj", "bound", "status", "iters")
+
+    def solve(self, options=None, warm=True, speculative=False):
+        """phgpu_solve into the output tensors (x, y, obj, bound, status, iters), or with
+        ``speculative`` into a second set that ``commit()`` swaps in and any other call
+        leaves unused (PHBase.iterk_loop launches the next solve before it knows whether
+        the convergence test stops the loop)."""
         o = options if options is not None else _lib.default_options()
+        if speculative:
+            if not hasattr(self, "_spec"):
+                self._spec = {k: torch.empty_like(getattr(self, k)) for k in self._OUTS}
+            out = self._spec
+        else:
+            out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
         rec = ins is not None and len(ins["events"]) < ins["iters"].shape[0]
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(self.x),
-                                        _ptr(self.y), _ptr(self.obj), _ptr(self.bound),
-                                        _ptr(self.status), _ptr(self.iters), self._stream()),
+        _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
+                                        _ptr(out["y"]), _ptr(out["obj"]), _ptr(out["bound"]),
+                                        _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
                    "phgpu_solve")
         if rec:
             ev[1].record()
-            ins["iters"][len(ins["events"])].copy_(self.iters)
+            ins["iters"][len(ins["events"])].copy_(out["iters"])
             ins["events"].append(ev)
+            ins.setdefault("spec", []).append(speculative)
+
+    def commit(self):
+        """Make the last speculative solve's outputs the current ones."""
+        for k in self._OUTS:
+            cur = getattr(self, k)
+            setattr(self, k, self._spec[k])
+            self._spec[k] = cur
+
+    def _status_counts(self):
+        if not hasattr(self, "_counts_dev"):
+            self._counts_dev = torch.zeros(4, dtype=torch.int32, device=self.device)
+            self._counts_host = torch.zeros(4, dtype=torch.int32).pin_memory()
+            self._counts_ev = torch.cuda.Event()
+        _lib.check(self.lib.phgpu_status_counts(self.h, _ptr(self.status), _ptr(self._counts_dev), self._stream()),
+                   "phgpu_status_counts")
 
     def count_not_optimal(self):
-        """Number of local scenarios whose last solve is not OPTIMAL (device count, one
-        scalar read back)."""
-        return int(torch.count_nonzero(self.status).item())
+        """Number of local scenarios whose last solve is not OPTIMAL (phgpu_status_counts,
+        one small read back)."""
+        self._status_counts()
+        c = self._counts_dev.cpu()
+        return int(c[1:].sum())
+
+    def count_not_optimal_async(self):
+        """Start the same count without waiting: the counts go to pinned host memory
+        behind an event; ``pending_not_optimal`` reads them (free after the next host
+        synchronisation)."""
+        self._status_counts()
+        self._counts_host.copy_(self._counts_dev, non_blocking=True)
+        self._counts_ev.record()
+
+    def pending_not_optimal(self):
+        self._counts_ev.synchronize()
+        return int(self._counts_host[1:].sum())
 
     def compute_xbar_partials(self):
         _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),
@@ -246,6 +288,20 @@ class PHEngine:
         """phbase.py:330-343: sum over ranks of per-rank means, / n_proc (host float)."""
         self.comm.allreduce_sum_(self.conv_buf)
         return float(self.conv_buf.item()) / self.comm.size
+
+    def convergence_diff_async(self):
+        """Start the same readback without waiting (pinned copy behind an event):
+        ``convergence_wait`` returns it; work queued after this call does not delay it."""
+        if not hasattr(self, "_conv_host"):
+            self._conv_host = torch.zeros(1, dtype=torch.float64).pin_memory()
+            self._conv_ev = torch.cuda.Event()
+        self.comm.allreduce_sum_(self.conv_buf)
+        self._conv_host.copy_(self.conv_buf, non_blocking=True)
+        self._conv_ev.record()
+
+    def convergence_wait(self):
+        self._conv_ev.synchronize()
+        return float(self._conv_host[0]) / self.comm.size
 
     def expectations(self):
         """(Eobj, Ebound, E1, Efeas, Eoptimal) summed over ranks (spopt.py:310-439)."""

@@ -102,12 +102,13 @@ class PHBase(SPOpt):
     # phbase.py:494-568 (dis_W / dis_prox wrappers around SPOpt.solve_loop)
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
                    dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
-                   tee=False, verbose=False, warm_start=True):
+                   tee=False, verbose=False, warm_start=True, speculative=False):
         wo, po = self.engine.W_on, self.engine.prox_on
         if dis_W or dis_prox:
             self.engine.set_terms(0 if dis_W else wo, 0 if dis_prox else po)
         super().solve_loop(solver_options, use_scenarios_not_subproblems, dtiming, gripe,
-                           disable_pyomo_signal_handling, tee, verbose, warm_start=warm_start)
+                           disable_pyomo_signal_handling, tee, verbose, warm_start=warm_start,
+                           speculative=speculative)
         if dis_W or dis_prox:
             self.engine.set_terms(wo, po)
 
@@ -211,6 +212,18 @@ class PHBase(SPOpt):
         return self.trivial_bound
 
     # phbase.py:875-979
+    def _speculate(self, have_ext):
+        if not self.options.get("speculative_solve", True):
+            return False
+        if self.options.get("display_timing") or self.options.get("record_pdhg_iters"):
+            return False
+        if self.ph_converger is not None:
+            return False
+        if have_ext and any(hasattr(self.extobject, h) for h in ("miditer", "pre_solve_loop", "post_solve_loop",
+                                                                  "pre_solve", "post_solve")):
+            return False
+        return True
+
     def iterk_loop(self):
         verbose = self.options["verbose"]
         have_ext = self.extensions is not None
@@ -225,7 +238,20 @@ class PHBase(SPOpt):
                 global_toc(f"\nInitiating PH Iteration {self._PHIter}\n", self.cylinder_rank == 0)
             self.Compute_Xbar(verbose)
             self.Update_W(verbose)
-            self.conv = self.convergence_diff()
+            # Speculative solve: the next solve_loop only depends on W and x̄, which are
+            # final here, so it is launched before the convergence readback and committed
+            # after the test (discarded when the loop stops) -- the GPU does not idle
+            # while the host reads conv and returns to launch the solve.  Off when an
+            # extension could change the problem between the test and the solve.
+            spec = self._speculate(have_ext)
+            if spec:
+                self.engine.convergence_diff_async()
+                self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
+                                gripe=False, verbose=verbose, speculative=True)
+                self.conv = self.engine.convergence_wait()
+            else:
+                self.conv = self.convergence_diff()
+            self.gripe_report()                        # the previous iteration's solves
             if have_ext and hasattr(self.extobject, "miditer"):
                 self.extobject.miditer()
             if self.ph_converger is not None:
@@ -239,8 +265,13 @@ class PHBase(SPOpt):
                 global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
                            % (self.conv, self.options["convthresh"]), self.cylinder_rank == 0)
                 break
-            self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming, gripe=True,
-                            verbose=verbose)
+            if spec:
+                self.engine.commit()
+                self.engine.count_not_optimal_async()  # its gripe, read at the next sync
+                self._gripe_pending = True
+            else:
+                self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
+                                gripe="deferred", verbose=verbose)
             if have_ext and hasattr(self.extobject, "enditer"):
                 self.extobject.enditer()
             if self.spcomm is not None:
@@ -258,9 +289,11 @@ class PHBase(SPOpt):
                 print("Iteration time: %6.2f" % (time.perf_counter() - t0))
                 print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
         else:
+            self.gripe_report()
             self.mpicomm.Barrier()
             global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations,
                        self.cylinder_rank == 0)
+        self.gripe_report()
 
     # phbase.py:982-1037
     def post_loops(self, extensions=None):

@@ -20,6 +20,10 @@ from .engine import PHEngine
 SOLVER_NAMES = ("mi355x_pdhg", "phgpu", "mi355x")
 
 
+# phgpu_options structs by their settings (built once: the PH loop solves with the same
+# options every iteration)
+_OPTIONS_CACHE = {}
+
 class SPOpt(SPBase):
     def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
                  all_nodenames=None, mpicomm=None, extensions=None, extension_kwargs=None,
@@ -53,16 +57,20 @@ class SPOpt(SPBase):
     @staticmethod
     def _to_phgpu_options(solver_options):
         so = {k: v for k, v in (solver_options or {}).items() if k not in SPOpt.FOREIGN_SOLVER_OPTIONS}
-        return _lib.default_options(**so)
+        key = tuple(sorted(so.items()))
+        o = _OPTIONS_CACHE.get(key)
+        if o is None:
+            o = _OPTIONS_CACHE[key] = _lib.default_options(**so)
+        return o
 
     # spopt.py:226-307
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
                    gripe=False, disable_pyomo_signal_handling=False, tee=False, verbose=False,
-                   warm_start=True):
+                   warm_start=True, speculative=False):
         if self.extensions is not None and hasattr(self.extobject, "pre_solve_loop"):
             self.extobject.pre_solve_loop()
         t0 = time.perf_counter()
-        self.engine.solve(self._to_phgpu_options(solver_options), warm=warm_start)
+        self.engine.solve(self._to_phgpu_options(solver_options), warm=warm_start, speculative=speculative)
         if dtiming or self.options.get("record_pdhg_iters", False):
             import torch
             torch.cuda.synchronize()
@@ -74,15 +82,31 @@ class SPOpt(SPBase):
         if dtiming and self.cylinder_rank == 0:
             print("Batched solve time (seconds): %4.4f  PDHG iters max/mean %d/%.1f"
                   % (self.solve_times[-1], *self.pdhg_iters[-1]))
-        if gripe and self.engine.count_not_optimal() > 0:
-            st = self.engine.status.cpu().numpy()
-            bad = np.nonzero((st != _lib.OPTIMAL) & (st != _lib.ITER_LIMIT))[0]
-            for k in bad[:10]:
-                print(f"Solve failed for scenario {self.batch.names[k]} (status {st[k]})")
-            lim = np.nonzero(st == _lib.ITER_LIMIT)[0]
-            if len(lim) and self.cylinder_rank == 0:
-                print(f"WARNING: {len(lim)} scenario(s) hit the PDHG iteration limit "
-                      f"(e.g. {self.batch.names[lim[0]]}); their solutions are approximate")
+        if gripe == "deferred":
+            # iterk_loop: the count is read at the next host synchronisation (the conv
+            # readback of the next PH iteration, or the end of the loop), not here
+            self.engine.count_not_optimal_async()
+            self._gripe_pending = True
+        elif gripe and self.engine.count_not_optimal() > 0:
+            self._gripe_print()
+
+    def gripe_report(self):
+        """The gripe of a solve_loop(gripe="deferred") (spopt.py:284-294 prints it right
+        after the solves; here it comes at the next synchronisation)."""
+        if getattr(self, "_gripe_pending", False):
+            self._gripe_pending = False
+            if self.engine.pending_not_optimal() > 0:
+                self._gripe_print()
+
+    def _gripe_print(self):
+        st = self.engine.status.cpu().numpy()
+        bad = np.nonzero((st != _lib.OPTIMAL) & (st != _lib.ITER_LIMIT))[0]
+        for k in bad[:10]:
+            print(f"Solve failed for scenario {self.batch.names[k]} (status {st[k]})")
+        lim = np.nonzero(st == _lib.ITER_LIMIT)[0]
+        if len(lim) and self.cylinder_rank == 0:
+            print(f"WARNING: {len(lim)} scenario(s) hit the PDHG iteration limit "
+                  f"(e.g. {self.batch.names[lim[0]]}); their solutions are approximate")
 
     # spopt.py:310-343 ("weighted, proxed" objective, phbase.py:991)
     def Eobjective(self, verbose=False):
