@@ -28,6 +28,7 @@
 
 #define WAVE 64
 #define BLOCK 64
+#define ORDER_BINS 256  // counting-sort bins of the longest-first work queue (solve_reg.inc)
 
 // ------------------------------------------------------------------ errors
 static thread_local char g_err[512] = {0};
@@ -108,6 +109,8 @@ struct phgpu_state {
     // wave w takes cw_slc[cw_ptr[w] .. cw_ptr[w+1]) (rw_* for rows)
     int32_t *cw_ptr, *cw_slc, *rw_ptr, *rw_slc;
     int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
+    int32_t* sk_bins;              // [2][ORDER_BINS] counting-sort histogram / fill counters (path 2)
+    int warm_rec;                  // the warm start lives in the records pk (paths 2r, 3), else in x / y
     double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
     int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
     // PH state (caller-owned)
@@ -1471,6 +1474,11 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     ALLOC(h->node_of, (size_t)depth * Sz);
     ALLOC(h->omega, Sz);
     h->shared = (flags & PHGPU_SHARED_MATRIX) ? 1 : 0;
+    // longest-first work queue (paths 2 and 4): iteration counts of the last solve, the
+    // queue order and the counting-sort bins
+    ALLOC(h->sk_iters, Sz);
+    ALLOC(h->sk_order, Sz);
+    ALLOC(h->sk_bins, 2 * ORDER_BINS);
     if (h->shared) {
         // one scaled matrix; iterates and per-scenario data live in the stream records
         // (allocated by phgpu_set_scenarios once the per-scenario column set is known)
@@ -1488,8 +1496,6 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         ALLOC(h->sh_u, n);
         ALLOC(h->sh_w, m);
         ALLOC(h->sh_part, (size_t)(n + 255) / 256 + 1);
-        ALLOC(h->sk_iters, Sz);
-        ALLOC(h->sk_order, Sz);
     } else {
         ALLOC(h->A, (size_t)nnz * Sz);
         ALLOC(h->c, (size_t)n * Sz);
@@ -1807,6 +1813,7 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
     h->have_solution = 0;
     h->scen_set = 1;
     h->last_path = 0;
+    h->warm_rec = 0;
     return 0;
 }
 
@@ -1843,6 +1850,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     h->have_solution = 0;
     h->scen_set = 1;
     h->last_path = 0;
+    h->warm_rec = 0;
     return 0;
 }
 
@@ -1950,13 +1958,10 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             HIPCHK(to_records(h, h->rho, h->nn, h->pk_RHO, st));
             HIPCHK(to_records(h, h->xbar, h->nn, h->pk_XB, st));
         }
-        if (P.warm && h->last_path != 3) {
+        if (P.warm && !h->warm_rec) {
             HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
             HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
         }
-    } else if (P.warm && h->last_path == 3) {
-        HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
-        HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
     }
     if (path == 3) {
         const wg_instance& gi = g_wg_instances[h->wg_inst];
@@ -1989,7 +1994,59 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         // outputs in the caller's scenario-fastest layout, unscaled
         HIPCHK(from_records(h, h->pk_X, h->pk_DC, h->n, x, st));
         if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
+        h->warm_rec = 1;
     } else if (use_reg) {
+        const int G = WAVE / h->reg_L;
+        const reg_instance& ri = g_reg_instances[h->reg_inst];
+        const size_t lds = (size_t)REG_WPB * reg_wave_lds(h->n, h->m, G, ri.KC, ri.KR) * sizeof(double);
+        // persistent grid: co-resident workgroups of REG_WPB independent waves (occupancy
+        // x CUs), never more than there are scenario groups
+        const int64_t need = (h->S + (int64_t)G * REG_WPB - 1) / ((int64_t)G * REG_WPB);
+        auto grid_of = [&](reg_kernel_t f, int& oc, int64_t& nb) -> hipError_t {
+            if (!oc) {
+                const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, (const void*)f,
+                                                                                  WAVE * REG_WPB, lds);
+                if (e != hipSuccess) return e;
+            }
+            nb = (int64_t)(oc < 1 ? 1 : oc) * h->num_cus;
+            if (nb > need) nb = need;
+            return hipSuccess;
+        };
+        int64_t nblk = 0;
+        HIPCHK(grid_of(ri.fn, h->occ_cache[2], nblk));
+        // record mode (solve_reg.inc, template REC) when groups take more than one scenario
+        // each: then the queue order matters (PHGPU_REG_REC=0|1 pins it)
+        const char* env = getenv("PHGPU_REG_REC");
+        const bool rec = env ? atoi(env) != 0 : nblk * REG_WPB * G < h->S;
+        const reg_kernel_t fn = rec ? ri.fn_rec : ri.fn;
+        if (rec) HIPCHK(grid_of(ri.fn_rec, h->occ_cache[6], nblk));
+        const int64_t first_dyn = nblk * REG_WPB * G;
+        if (rec) {
+            if (!h->pk) {
+                const int rc3 = pack_alloc(h);
+                if (rc3) return rc3;
+                if (h->scen_set) HIPCHK(pack_fill(h, st));
+            }
+            if (h->W_on) HIPCHK(to_records(h, h->W, h->nn, h->pk_W, st));
+            if (h->prox_on) {
+                HIPCHK(to_records(h, h->rho, h->nn, h->pk_RHO, st));
+                HIPCHK(to_records(h, h->xbar, h->nn, h->pk_XB, st));
+            }
+            if (P.warm && !h->warm_rec) {
+                HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
+                HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
+            }
+            if (!h->have_solution) HIPCHK(hipMemsetAsync(h->sk_iters, 0, (size_t)h->S * sizeof(int32_t), st));
+            HIPCHK(hipMemsetAsync(h->sk_bins, 0, 2 * ORDER_BINS * sizeof(int32_t), st));
+            const dim3 ob((unsigned)((h->S + ORDER_BINS - 1) / ORDER_BINS));
+            hipLaunchKernelGGL(k_reg_hist, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every,
+                               h->sk_bins);
+            hipLaunchKernelGGL(k_reg_order, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every,
+                               h->sk_bins, h->sk_order);
+        } else if (P.warm && h->warm_rec) {
+            HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
+            HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
+        }
         reg_plan pl;
         pl.L = h->reg_L;
         pl.kc = h->reg_kc;
@@ -2000,26 +2057,25 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.col_r = h->pl_col_r;
         pl.row_k = h->pl_row_k;
         pl.row_c = h->pl_row_c;
-        const int G = WAVE / pl.L;
-        const reg_instance& ri = g_reg_instances[h->reg_inst];
-        const size_t lds = (size_t)REG_WPB * reg_wave_lds(h->n, h->m, G, ri.KC, ri.KR) * sizeof(double);
-        const reg_kernel_t fn = g_reg_instances[h->reg_inst].fn;
-        // persistent grid: co-resident workgroups of REG_WPB independent waves (occupancy
-        // x CUs), never more than there are scenario groups
-        int per_cu = 0;
-        int& oc = h->occ_cache[2];
-        if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, (const void*)fn, WAVE * REG_WPB, lds));
-        per_cu = oc;
-        if (per_cu < 1) per_cu = 1;
-        const int64_t need = (h->S + (int64_t)G * REG_WPB - 1) / ((int64_t)G * REG_WPB);
-        int64_t nblk = (int64_t)per_cu * h->num_cus;
-        if (nblk > need) nblk = need;
-        const int64_t first_dyn = nblk * REG_WPB * G;
+        pl.order = h->sk_order;
+        pl.last_iters = h->sk_iters;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
         hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE * REG_WPB), lds, st, *h, P, pl, h->qhead, first_dyn,
                            x, y, obj, bound, status, iters);
+        HIPCHK(hipGetLastError());
+        if (rec) {
+            // outputs in the caller's scenario-fastest layout, unscaled
+            HIPCHK(from_records(h, h->pk_X, h->pk_DC, h->n, x, st));
+            if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
+        }
+        h->warm_rec = rec ? 1 : 0;
     } else {
+        if (P.warm && h->warm_rec) {
+            HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
+            HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
+        }
         hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+        h->warm_rec = 0;
     }
     HIPCHK(hipGetLastError());
     h->have_solution = 1;
@@ -2124,7 +2180,7 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->pk, h->cmap, h->rmap, h->pcol, h->prow, h->sh_col, h->sh_row, h->sh_norm, h->sh_v,
                     h->sh_u, h->sh_w, h->sh_part, h->sk, h->cs_off, h->cs_len, h->cs_idx, h->cs_src,
                     h->rs_off, h->rs_len, h->rs_idx, h->rs_src, h->cs_val, h->rs_val, h->sk_iters, h->sk_order,
-                    h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
+                    h->sk_bins, h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
