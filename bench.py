@@ -201,7 +201,8 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
     n, m, nnz, nn = b.n, b.m, b.nnz, b.nn
     path = kinfo["path"]
     if path == 2:
-        kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}>"
+        rec = "true" if kinfo.get("rec") == 1 else "false"
+        kname = f"k_solve_reg<{kinfo['KC']}, {kinfo['ZC']}, {kinfo['KR']}, {kinfo['ZR']}, {rec}>"
         lanes = kinfo["lanes"]
     elif path == 3:
         kname = f"k_solve_wg<{kinfo['wKC']}, {kinfo['wZC']}, {kinfo['wKR']}, {kinfo['wZR']}, {kinfo['wps']}>"

@@ -209,12 +209,13 @@ int phgpu_last_error(char* buf, size_t len);
 /* Workspace bytes held by the handle (diagnostics / memory planning). */
 int64_t phgpu_workspace_bytes(phgpu_handle h);
 
-/* Solve-kernel selection of the handle (diagnostics): info[17] =
+/* Solve-kernel selection of the handle (diagnostics): info[18] =
  * {register path (L <= 64 lanes per scenario): instance or -1, L, column slots / CSC
  *  entries per column / row slots / CSR entries per row needed, the instance's KC, ZC, KR,
  *  ZR;  workgroup path (one workgroup per scenario): instance or -1, waves per scenario,
  *  KC, ZC, KR, ZR;  the default path of phgpu_solve: 1 global, 2 register, 3 workgroup,
- *  4 shared-matrix streaming}. */
+ *  4 shared-matrix streaming;  the queue mode of the last register-path solve: 1 record
+ *  mode (longest-first queue, scenario-major records), 0 scenario order, -1 none yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
 #ifdef __cplusplus

@@ -109,8 +109,10 @@ struct phgpu_state {
     // wave w takes cw_slc[cw_ptr[w] .. cw_ptr[w+1]) (rw_* for rows)
     int32_t *cw_ptr, *cw_slc, *rw_ptr, *rw_slc;
     int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
-    int32_t* sk_bins;              // [2][ORDER_BINS] counting-sort histogram / fill counters (path 2)
+    int32_t* sk_bins;              // [2 parities][2][ORDER_BINS] counting-sort histogram / fill counters (path 2)
+    int order_parity;              // which half of sk_bins the next register-path solve uses
     int warm_rec;                  // the warm start lives in the records pk (paths 2r, 3), else in x / y
+    int last_rec;                  // queue mode of the last register-path solve (-1 none yet)
     double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
     int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
     // PH state (caller-owned)
@@ -468,6 +470,35 @@ __global__ void __launch_bounds__(256) k_to_records(const double* __restrict__ i
         const int64_t s = s0 + r;
         const int k = k0 + tx;
         if (s < S && k < K) pk[(size_t)s * (size_t)stride + off + k] = tile[tx][r];
+    }
+}
+
+// the PH state of a solve into the records in one launch: W | rho | xbar are consecutive
+// record fields of nn entries each (pk_W, pk_RHO, pk_XB); a null source is skipped
+__global__ void __launch_bounds__(256) k_to_records_ph(const double* __restrict__ W, const double* __restrict__ rho,
+                                                       const double* __restrict__ xbar, int nn, int64_t S,
+                                                       double* __restrict__ pk, int64_t stride, int off) {
+    __shared__ double tile[TT][TT + 1];
+    const int64_t s0 = (int64_t)blockIdx.x * TT;
+    const int k0 = blockIdx.y * TT;
+    const int K = 3 * nn;
+    const int tx = threadIdx.x % TT, ty = threadIdx.x / TT;
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int k = k0 + r;
+        const int64_t s = s0 + tx;
+        const int part = k < nn ? 0 : (k < 2 * nn ? 1 : 2);
+        const double* a = part == 0 ? W : (part == 1 ? rho : xbar);
+        double v = 0.0;
+        if (k < K && a && s < S) v = a[(size_t)(k - part * nn) * (size_t)S + (size_t)s];
+        tile[r][tx] = v;
+    }
+    __syncthreads();
+    for (int r = ty; r < TT; r += 256 / TT) {
+        const int64_t s = s0 + r;
+        const int k = k0 + tx;
+        const int part = k < nn ? 0 : (k < 2 * nn ? 1 : 2);
+        const bool have = part == 0 ? W != nullptr : (part == 1 ? rho != nullptr : xbar != nullptr);
+        if (s < S && k < K && have) pk[(size_t)s * (size_t)stride + off + k] = tile[tx][r];
     }
 }
 
@@ -1221,6 +1252,16 @@ static hipError_t to_records(phgpu_state* h, const double* in, int K, int off, h
     return hipGetLastError();
 }
 
+// this solve's PH state (W if on, rho and xbar if the prox term is on) into the records
+static hipError_t ph_to_records(phgpu_state* h, hipStream_t st) {
+    if (h->nn <= 0 || (!h->W_on && !h->prox_on)) return hipSuccess;
+    const dim3 g((unsigned)((h->S + TT - 1) / TT), (unsigned)((3 * h->nn + TT - 1) / TT));
+    hipLaunchKernelGGL(k_to_records_ph, g, dim3(256), 0, st, h->W_on ? h->W : nullptr,
+                       h->prox_on ? h->rho : nullptr, h->prox_on ? h->xbar : nullptr, h->nn, h->S, h->pk,
+                       h->pk_stride, h->pk_W);
+    return hipGetLastError();
+}
+
 static hipError_t from_records(phgpu_state* h, int off, int moff, int K, double* out, hipStream_t st) {
     if (K <= 0 || !out) return hipSuccess;
     const dim3 g((unsigned)((h->S + TT - 1) / TT), (unsigned)((K + TT - 1) / TT));
@@ -1427,6 +1468,7 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         return set_err(-3, "out of host memory");
     }
     memset(h, 0, sizeof(*h));
+    h->last_rec = -1;
     h->device = device;
     h->S = S;
     h->n = n;
@@ -1478,7 +1520,11 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     // queue order and the counting-sort bins
     ALLOC(h->sk_iters, Sz);
     ALLOC(h->sk_order, Sz);
-    ALLOC(h->sk_bins, 2 * ORDER_BINS);
+    ALLOC(h->sk_bins, 4 * ORDER_BINS);
+    if (hipMemset(h->sk_bins, 0, 4 * ORDER_BINS * sizeof(int32_t)) != hipSuccess) {
+        phgpu_destroy(h);
+        return set_err(-2, "hipMemset failed");
+    }
     if (h->shared) {
         // one scaled matrix; iterates and per-scenario data live in the stream records
         // (allocated by phgpu_set_scenarios once the per-scenario column set is known)
@@ -1953,11 +1999,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
     }
     if (path == 3) {
         // this solve's PH state into the records; a warm start left by another path too
-        if (h->W_on) HIPCHK(to_records(h, h->W, h->nn, h->pk_W, st));
-        if (h->prox_on) {
-            HIPCHK(to_records(h, h->rho, h->nn, h->pk_RHO, st));
-            HIPCHK(to_records(h, h->xbar, h->nn, h->pk_XB, st));
-        }
+        HIPCHK(ph_to_records(h, st));
         if (P.warm && !h->warm_rec) {
             HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
             HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
@@ -2027,22 +2069,19 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
                 if (rc3) return rc3;
                 if (h->scen_set) HIPCHK(pack_fill(h, st));
             }
-            if (h->W_on) HIPCHK(to_records(h, h->W, h->nn, h->pk_W, st));
-            if (h->prox_on) {
-                HIPCHK(to_records(h, h->rho, h->nn, h->pk_RHO, st));
-                HIPCHK(to_records(h, h->xbar, h->nn, h->pk_XB, st));
-            }
+            HIPCHK(ph_to_records(h, st));
             if (P.warm && !h->warm_rec) {
                 HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
                 HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
             }
             if (!h->have_solution) HIPCHK(hipMemsetAsync(h->sk_iters, 0, (size_t)h->S * sizeof(int32_t), st));
-            HIPCHK(hipMemsetAsync(h->sk_bins, 0, 2 * ORDER_BINS * sizeof(int32_t), st));
             const dim3 ob((unsigned)((h->S + ORDER_BINS - 1) / ORDER_BINS));
-            hipLaunchKernelGGL(k_reg_hist, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every,
-                               h->sk_bins);
-            hipLaunchKernelGGL(k_reg_order, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every,
-                               h->sk_bins, h->sk_order);
+            int32_t* bins = h->sk_bins + 2 * ORDER_BINS * h->order_parity;
+            int32_t* other = h->sk_bins + 2 * ORDER_BINS * (1 - h->order_parity);
+            h->order_parity ^= 1;
+            hipLaunchKernelGGL(k_reg_hist, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins);
+            hipLaunchKernelGGL(k_reg_order, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins,
+                               other, h->sk_order);
         } else if (P.warm && h->warm_rec) {
             HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
             HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
@@ -2059,6 +2098,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_c = h->pl_row_c;
         pl.order = h->sk_order;
         pl.last_iters = h->sk_iters;
+        pl.ema = h->have_solution ? 1 : 0;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
         hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE * REG_WPB), lds, st, *h, P, pl, h->qhead, first_dyn,
                            x, y, obj, bound, status, iters);
@@ -2069,6 +2109,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
         }
         h->warm_rec = rec ? 1 : 0;
+        h->last_rec = rec ? 1 : 0;
     } else {
         if (P.warm && h->warm_rec) {
             HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
@@ -2125,16 +2166,34 @@ extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const doubl
 }
 
 // counts[c] = number of local scenarios with status c (c = 0..3), one block
-__global__ void __launch_bounds__(1024) k_status_counts(const int32_t* __restrict__ status, int64_t S,
+// counts[k] = #{s : status[s] == k}: one block, four statuses per load, several loads in
+// flight per thread (a device-wide "last block" reduction needs a release fence, i.e. an
+// L2 writeback of every XCD, which costs more than the whole count)
+#define SC_T 1024
+__global__ void __launch_bounds__(SC_T) k_status_counts(const int32_t* __restrict__ status, int64_t S,
                                                         int32_t* __restrict__ counts) {
     __shared__ int32_t c[4];
     if (threadIdx.x < 4) c[threadIdx.x] = 0;
     __syncthreads();
     int32_t loc[4] = {0, 0, 0, 0};
-    for (int64_t s = threadIdx.x; s < S; s += 1024) {
-        const int32_t v = status[s];
-        if (v >= 0 && v < 4) ++loc[v];
+    // (a macro, not a lambda: a by-reference capture of loc[] would put it in scratch)
+#define SC_ADD(v) loc[0] += (v) == 0, loc[1] += (v) == 1, loc[2] += (v) == 2, loc[3] += (v) == 3
+    const int64_t S4 = ((uintptr_t)status % 16 == 0) ? S / 4 : 0;  // int4 part
+    const int4* s4 = (const int4*)status;
+    int64_t i = threadIdx.x;
+    for (; i + 3 * SC_T < S4; i += 4 * SC_T) {
+        const int4 a = s4[i], b = s4[i + SC_T], d = s4[i + 2 * SC_T], e = s4[i + 3 * SC_T];
+        SC_ADD(a.x); SC_ADD(a.y); SC_ADD(a.z); SC_ADD(a.w);
+        SC_ADD(b.x); SC_ADD(b.y); SC_ADD(b.z); SC_ADD(b.w);
+        SC_ADD(d.x); SC_ADD(d.y); SC_ADD(d.z); SC_ADD(d.w);
+        SC_ADD(e.x); SC_ADD(e.y); SC_ADD(e.z); SC_ADD(e.w);
     }
+    for (; i < S4; i += SC_T) {
+        const int4 a = s4[i];
+        SC_ADD(a.x); SC_ADD(a.y); SC_ADD(a.z); SC_ADD(a.w);
+    }
+    for (int64_t t = 4 * S4 + threadIdx.x; t < S; t += SC_T) SC_ADD(status[t]);
+#undef SC_ADD
     for (int k = 0; k < 4; ++k)
         if (loc[k]) atomicAdd(&c[k], loc[k]);
     __syncthreads();
@@ -2143,7 +2202,7 @@ __global__ void __launch_bounds__(1024) k_status_counts(const int32_t* __restric
 
 extern "C" int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_t* counts, void* stream) {
     if (!h || !status || !counts) return set_err(-1, "null argument");
-    hipLaunchKernelGGL(k_status_counts, dim3(1), dim3(1024), 0, (hipStream_t)stream, status, h->S, counts);
+    hipLaunchKernelGGL(k_status_counts, dim3(1), dim3(SC_T), 0, (hipStream_t)stream, status, h->S, counts);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2199,8 +2258,10 @@ extern "C" int64_t phgpu_workspace_bytes(phgpu_handle h) { return h ? h->ws_byte
 extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     if (!h || !info) return set_err(-1, "null argument");
     // info[0..9]: the register path (L <= 64); info[10..15]: the workgroup path; info[16]:
-    // the path phgpu_solve takes by default (1 global, 2 register, 3 workgroup)
-    for (int k = 0; k < 17; ++k) info[k] = 0;
+    // the path phgpu_solve takes by default (1 global, 2 register, 3 workgroup); info[17]:
+    // queue mode of the last register-path solve (1 record mode, 0 scenario order, -1 none)
+    for (int k = 0; k < 18; ++k) info[k] = 0;
+    info[17] = h->last_rec;
     info[0] = h->reg_inst;
     info[1] = h->reg_inst >= 0 ? h->reg_L : 0;
     info[2] = h->reg_kc;

@@ -120,6 +120,9 @@ class PHEngine:
         self.xfix = None
         self.W_on = 0
         self.prox_on = 0
+        # row duals are an optional phgpu_solve output: PH never reads them, so the hot
+        # loop leaves them on the device side (set True to have ``y`` filled by solves)
+        self.want_duals = False
         self._upload()
 
     # -------------------------------------------------------------- plumbing
@@ -154,10 +157,10 @@ class PHEngine:
 
     def kernel_info(self):
         """Which solve kernel the handle uses (phgpu_kernel_info)."""
-        info = (ctypes.c_int32 * 17)()
+        info = (ctypes.c_int32 * 18)()
         _lib.check(self.lib.phgpu_kernel_info(self.h, info), "phgpu_kernel_info")
         keys = ["instance", "lanes", "kc", "zc", "kr", "zr", "KC", "ZC", "KR", "ZR",
-                "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path"]
+                "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path", "rec"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state
@@ -224,7 +227,8 @@ class PHEngine:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
-                                        _ptr(out["y"]), _ptr(out["obj"]), _ptr(out["bound"]),
+                                        _ptr(out["y"] if self.want_duals else None), _ptr(out["obj"]),
+                                        _ptr(out["bound"]),
                                         _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
                    "phgpu_solve")
         if rec:

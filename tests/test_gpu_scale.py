@@ -69,6 +69,8 @@ def test_headline_farmer65536_cm1(gpu):
     info = ph.engine.kernel_info()
     assert info["lanes"] == 4 and (info["KC"], info["ZC"], info["KR"], info["ZR"]) == (3, 3, 2, 4), info
     _run_and_compare(ph, g)
+    # the bench's queue mode: scenario-major records, longest-first queue
+    assert ph.engine.kernel_info()["rec"] == 1
 
 
 def test_config2_farmer1024_cm10_bound(gpu):
