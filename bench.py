@@ -58,6 +58,8 @@ def parse():
                    help="PDHG eps_rel of the PH solves (default 1e-9; uc: 1e-6 for Iter0 and PH)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                    help="torch.distributed backend for N > 1 (auto: RCCL when every rank has its own GPU)")
+    p.add_argument("--solver-opt", action="append", default=[], metavar="KEY=VALUE",
+                   help="extra phgpu_options for the PH solves (tuning), e.g. check_every=32")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     p.add_argument("--profile-dir", default=None,
@@ -373,6 +375,9 @@ def main():
             "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
             "device": f"cuda:{dev_index}",
             "iterk_solver_options": {"eps_rel": a.eps}}
+    for kv in a.solver_opt:
+        k, v = kv.split("=", 1)
+        opts["iterk_solver_options"][k] = float(v) if any(ch in v for ch in ".e") else int(v)
     t_setup = time.perf_counter()
     if a.model == "farmer":
         names = farmer.scenario_names_creator(a.scens)

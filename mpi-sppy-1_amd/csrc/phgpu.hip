@@ -1065,7 +1065,9 @@ static inline long reg_cost(const reg_instance& r) {
 // SIMD is skipped by the lane search (L doubles past it).  Measured on farmer 65,536 cm=1
 // (profiles/r01): <8,4,4,4> at L=2 spills 1.5 KB -> 14.4 ms per solve; <3,3,2,4> at L=4
 // spills 68 B -> 0.67 ms; <2,3,1,4> at L=8, no spill -> 0.77 ms.
+#ifndef REG_SPILL_MAX
 #define REG_SPILL_MAX 128
+#endif
 static bool reg_spills(const reg_instance& r) {
     hipFuncAttributes a;
     if (hipFuncGetAttributes(&a, (const void*)r.fn) != hipSuccess) return false;
