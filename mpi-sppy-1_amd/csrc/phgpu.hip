@@ -2083,7 +2083,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             h->order_parity ^= 1;
             hipLaunchKernelGGL(k_reg_hist, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins);
             hipLaunchKernelGGL(k_reg_order, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins,
-                               other, h->sk_order);
+                               other, h->sk_order, h->qhead);
         } else if (P.warm && h->warm_rec) {
             HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
             HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
@@ -2101,7 +2101,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.order = h->sk_order;
         pl.last_iters = h->sk_iters;
         pl.ema = h->have_solution ? 1 : 0;
-        HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
+        if (!rec) HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));  // record mode: k_reg_order did
         hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE * REG_WPB), lds, st, *h, P, pl, h->qhead, first_dyn,
                            x, y, obj, bound, status, iters);
         HIPCHK(hipGetLastError());
