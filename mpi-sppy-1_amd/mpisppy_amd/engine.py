@@ -194,8 +194,7 @@ class PHEngine:
         iteration counts (one D2D copy after the launch, outside the event pair).  Used
         by bench.py for the per-launch roofline inside its timed region."""
         self._ins = {"events": [], "iters": torch.empty((max_solves, self.S), dtype=torch.int32,
-                                                         device=self.device),
-                     "side": torch.cuda.Stream(device=self.device)}
+                                                         device=self.device)}
 
     def instrumented(self):
         """[(launch ms, scenario-iterations)] of the recorded launches (syncs)."""
@@ -203,7 +202,6 @@ class PHEngine:
         if not ins:
             return []
         torch.cuda.synchronize(self.device)
-        ins["side"].synchronize()
         k = len(ins["events"])
         its = ins["iters"][:k].sum(dim=1, dtype=torch.int64).cpu().tolist()
         return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
@@ -225,9 +223,6 @@ class PHEngine:
             out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
         rec = ins is not None and len(ins["events"]) < ins["iters"].shape[0]
-        if ins is not None and "snap" in ins:
-            # the output set this solve writes may still be read by the last snapshot copy
-            torch.cuda.current_stream(self.device).wait_event(ins["snap"])
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -238,16 +233,7 @@ class PHEngine:
                    "phgpu_solve")
         if rec:
             ev[1].record()
-            # the snapshot copy runs on a side stream behind the launch's end event, so the
-            # timed loop does not wait for it; the next solve writes the other output set
-            # (speculative solves alternate two), and a non-speculative one waits for it
-            side = ins["side"]
-            side.wait_event(ev[1])
-            with torch.cuda.stream(side):
-                ins["iters"][len(ins["events"])].copy_(out["iters"])
-            snap = torch.cuda.Event()
-            snap.record(side)
-            ins["snap"] = snap
+            ins["iters"][len(ins["events"])].copy_(out["iters"])
             ins["events"].append(ev)
             ins.setdefault("spec", []).append(speculative)
 

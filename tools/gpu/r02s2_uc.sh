@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 2 (session 2): verify the queue-head reset / side-stream snapshot on config 3, GPU
+# suite; config 5 (UC, 1,000 scenarios) with the EMA queue key for path 4.
+cd "$(dirname "$0")/../.." || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+    local name=$1 secs=$2; shift 2
+    echo "=== $name (limit ${secs}s)"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -1 "gpurun_out/$name.log" | cut -c1-200
+    if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+B="python3 -u bench.py --no-cpu-baseline"
+step u_bench_cfg3 300 $B
+step u_gputests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step u_bench_uc 900 $B --model uc --scens 1000 --steps 2 --warmup 1
+echo done
