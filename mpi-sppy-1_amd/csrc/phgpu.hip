@@ -114,7 +114,7 @@ struct phgpu_state {
     int warm_rec;                  // the warm start lives in the records pk (paths 2r, 3), else in x / y
     int last_rec;                  // queue mode of the last register-path solve (-1 none yet)
     double* sk;  // stream records: X X0 U XT | Y Y0 YT | PC (8 per P column) | PR (4 per R row)
-    int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_YF, sk_PC, sk_PR, sk_cap;
+    int64_t sk_stride, sk_X, sk_X0, sk_U, sk_XT, sk_Y, sk_Y0, sk_YT, sk_PC, sk_PR, sk_cap;
     // PH state (caller-owned)
     const double *W, *rho, *xbar;
     int W_on, prox_on;
@@ -1836,7 +1836,6 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
     h->sk_Y = o; o += al(m);
     h->sk_Y0 = o; o += al(m);
     h->sk_YT = o; o += al(m);
-    h->sk_YF = o; o += al((m + 1) / 2);  // fp32 copy of Y (F32 gathers)
     h->sk_PC = o; o += al(8 * (int64_t)h->np);
     h->sk_PR = o; o += al(4 * (int64_t)h->nr);
     h->sk_stride = o;
@@ -1961,12 +1960,8 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         // B scenario slots per workgroup (PHGPU_STREAM_SLOTS=1|2, default 2)
         const char* env = getenv("PHGPU_STREAM_SLOTS");
         const int B = (env && atoi(env) == 1) ? 1 : 2;
-        // fp32 gathered vectors (PHGPU_STREAM_F32=1; k_solve_stream)
-        const char* env32 = getenv("PHGPU_STREAM_F32");
-        const bool f32 = env32 && atoi(env32) == 1;
-        const void* fn = B == 1 ? (f32 ? (const void*)k_solve_stream<1, true> : (const void*)k_solve_stream<1, false>)
-                                : (f32 ? (const void*)k_solve_stream<2, true> : (const void*)k_solve_stream<2, false>);
-        int& oc = h->occ_cache[f32 ? (B == 1 ? 0 : 7) : (B == 1 ? 4 : 5)];
+        const void* fn = B == 1 ? (const void*)k_solve_stream<1> : (const void*)k_solve_stream<2>;
+        int& oc = h->occ_cache[B == 1 ? 4 : 5];
         if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, SBLK, 0));
         per_cu = oc;
         if (per_cu < 1) per_cu = 1;
@@ -1981,10 +1976,10 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         else
             hipLaunchKernelGGL(k_stream_order_identity, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
         if (B == 1)
-            hipLaunchKernelGGL((f32 ? k_solve_stream<1, true> : k_solve_stream<1, false>), dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+            hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters);
         else
-            hipLaunchKernelGGL((f32 ? k_solve_stream<2, true> : k_solve_stream<2, false>), dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+            hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters);
         HIPCHK(hipGetLastError());
         h->have_solution = 1;
