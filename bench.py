@@ -60,6 +60,8 @@ def parse():
                    help="torch.distributed backend for N > 1 (auto: RCCL when every rank has its own GPU)")
     p.add_argument("--solver-opt", action="append", default=[], metavar="KEY=VALUE",
                    help="extra phgpu_options for the PH solves (tuning), e.g. check_every=32")
+    p.add_argument("--default-solver-options", action="store_true",
+                   help="farmer: ignore the example's recommended PH-solve options (library defaults)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     p.add_argument("--profile-dir", default=None,
@@ -375,6 +377,9 @@ def main():
             "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
             "device": f"cuda:{dev_index}",
             "iterk_solver_options": {"eps_rel": a.eps}}
+    if a.model == "farmer" and not a.default_solver_options:
+        # the example's recommended PH-solve options (examples/farmer.py PDHG_ITERK_OPTIONS)
+        opts["iterk_solver_options"].update(farmer.PDHG_ITERK_OPTIONS)
     for kv in a.solver_opt:
         k, v = kv.split("=", 1)
         opts["iterk_solver_options"][k] = float(v) if any(ch in v for ch in ".e") else int(v)
@@ -463,7 +468,10 @@ def main():
             "config": {"workload": workload, "scenarios": a.scens,
                        "crops_multiplier": a.cm if a.model == "farmer" else None,
                        "tree_nodes": len(b.node_names),
-                       "rho": a.rho, "eps_rel": a.eps, "scenarios_per_gpu": b.S,
+                       "rho": a.rho, "eps_rel": a.eps,
+                       "iterk_solver_options": {k: v for k, v in opts["iterk_solver_options"].items()
+                                                if k != "eps_rel"},
+                       "scenarios_per_gpu": b.S,
                        "n": b.n, "m": b.m, "nnz": b.nnz,
                        "parallelism": (f"scenario-sharded x{world}" +
                                        (f" ({'RCCL' if backend == 'nccl' else 'gloo, ranks sharing a GPU'}"
