@@ -475,12 +475,12 @@ __global__ void __launch_bounds__(256) k_to_records(const double* __restrict__ i
 
 // the PH state of a solve into the records in one launch: W | rho | xbar are consecutive
 // record fields of nn entries each (pk_W, pk_RHO, pk_XB); a null source is skipped
-__global__ void __launch_bounds__(256) k_to_records_ph(const double* __restrict__ W, const double* __restrict__ rho,
-                                                       const double* __restrict__ xbar, int nn, int64_t S,
-                                                       double* __restrict__ pk, int64_t stride, int off) {
-    __shared__ double tile[TT][TT + 1];
-    const int64_t s0 = (int64_t)blockIdx.x * TT;
-    const int k0 = blockIdx.y * TT;
+__device__ __forceinline__ void to_records_ph_tile(double (*tile)[TT + 1], int bx, int by, const double* __restrict__ W,
+                                                   const double* __restrict__ rho, const double* __restrict__ xbar,
+                                                   int nn, int64_t S, double* __restrict__ pk, int64_t stride,
+                                                   int off) {
+    const int64_t s0 = (int64_t)bx * TT;
+    const int k0 = by * TT;
     const int K = 3 * nn;
     const int tx = threadIdx.x % TT, ty = threadIdx.x / TT;
     for (int r = ty; r < TT; r += 256 / TT) {
@@ -500,6 +500,13 @@ __global__ void __launch_bounds__(256) k_to_records_ph(const double* __restrict_
         const bool have = part == 0 ? W != nullptr : (part == 1 ? rho != nullptr : xbar != nullptr);
         if (s < S && k < K && have) pk[(size_t)s * (size_t)stride + off + k] = tile[tx][r];
     }
+}
+
+__global__ void __launch_bounds__(256) k_to_records_ph(const double* __restrict__ W, const double* __restrict__ rho,
+                                                       const double* __restrict__ xbar, int nn, int64_t S,
+                                                       double* __restrict__ pk, int64_t stride, int off) {
+    __shared__ double tile[TT][TT + 1];
+    to_records_ph_tile(tile, blockIdx.x, blockIdx.y, W, rho, xbar, nn, S, pk, stride, off);
 }
 
 // out[k][s] = pk[s][off + k] * (moff >= 0 ? pk[s][moff + k] : 1)
@@ -2071,7 +2078,6 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
                 if (rc3) return rc3;
                 if (h->scen_set) HIPCHK(pack_fill(h, st));
             }
-            HIPCHK(ph_to_records(h, st));
             if (P.warm && !h->warm_rec) {
                 HIPCHK(to_records(h, h->x, h->n, h->pk_X, st));
                 HIPCHK(to_records(h, h->y, h->m, h->pk_Y, st));
@@ -2081,7 +2087,14 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             int32_t* bins = h->sk_bins + 2 * ORDER_BINS * h->order_parity;
             int32_t* other = h->sk_bins + 2 * ORDER_BINS * (1 - h->order_parity);
             h->order_parity ^= 1;
-            hipLaunchKernelGGL(k_reg_hist, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins);
+            // histogram + this solve's PH state into the records, one launch (k_reg_prep)
+            const bool ph = h->nn > 0 && (h->W_on || h->prox_on);
+            const int nh = (int)ob.x;
+            const int gx = (int)((h->S + TT - 1) / TT), gy = ph ? (3 * h->nn + TT - 1) / TT : 0;
+            hipLaunchKernelGGL(k_reg_prep, dim3((unsigned)(nh + gx * gy)), dim3(256), 0, st, h->sk_iters, h->S,
+                               P.restart_every, bins, nh, gx, h->W_on ? h->W : nullptr,
+                               h->prox_on ? h->rho : nullptr, h->prox_on ? h->xbar : nullptr, h->nn, h->pk,
+                               h->pk_stride, h->pk_W);
             hipLaunchKernelGGL(k_reg_order, ob, dim3(ORDER_BINS), 0, st, h->sk_iters, h->S, P.restart_every, bins,
                                other, h->sk_order, h->qhead);
         } else if (P.warm && h->warm_rec) {
