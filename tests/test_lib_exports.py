@@ -57,6 +57,12 @@ def test_host_only_calls(lib):
     assert L.phgpu_workspace_bytes(None) == -1
     with pytest.raises(KeyError):
         _lib.default_options(nonsense=1)
+    # the library keeps PDLP's restart constants; farmer's recommended PH-solve options
+    # (examples/farmer.py, used by bench.py) are valid phgpu_options fields
+    assert o.beta_sufficient == 0.2 and o.beta_necessary == 0.8 and o.beta_artificial == 0.36
+    from mpisppy_amd.examples import farmer
+    of = _lib.default_options(**farmer.PDHG_ITERK_OPTIONS)
+    assert of.beta_sufficient == farmer.PDHG_ITERK_OPTIONS["beta_sufficient"]
 
 
 def test_product_path_has_no_cpu_fallback():
