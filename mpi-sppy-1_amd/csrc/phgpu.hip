@@ -1069,16 +1069,27 @@ static inline long reg_cost(const reg_instance& r) {
 }
 
 // an instance that spills more than REG_SPILL_MAX bytes of scratch per lane at 2 waves /
-// SIMD is skipped by the lane search (L doubles past it).  Measured on farmer 65,536 cm=1
-// (profiles/r01): <8,4,4,4> at L=2 spills 1.5 KB -> 14.4 ms per solve; <3,3,2,4> at L=4
-// spills 68 B -> 0.67 ms; <2,3,1,4> at L=8, no spill -> 0.77 ms.
+// SIMD is skipped by the lane search (L doubles past it).  Both variants are checked --
+// scenario order (fn) and record mode (fn_rec), whichever phgpu_solve will launch.
+// Measured on farmer 65,536 cm=1 (profiles/r01): <8,4,4,4> at L=2 spills 1.5 KB -> 14.4 ms
+// per solve; <2,3,1,4> at L=8, no spill -> 0.77 ms.  <3,3,2,4> (the headline instance)
+// spills 28 B (fn) / 268 B (fn_rec), all of it outside the PDHG step loop: the scratch
+// operations of its code object sit in the prologue, the scenario load / refill, the check
+// iteration and the write-back, none in the R-1 plain steps (tools/scratch_regions.py,
+// profiles/r03/scratch_regions.txt) -- so the cap sits above 268 B.  The first instance
+// whose step loop spills is <6,4,2,4> (568 / 940 B, 43 / 37 scratch ops in the loop);
+// <4,4,2,4> (216 / 508 B) keeps its loop clean but spills 98 / 174 times in the check and
+// refill paths, and stays excluded as before.
 #ifndef REG_SPILL_MAX
-#define REG_SPILL_MAX 128
+#define REG_SPILL_MAX 320
 #endif
 static bool reg_spills(const reg_instance& r) {
-    hipFuncAttributes a;
-    if (hipFuncGetAttributes(&a, (const void*)r.fn) != hipSuccess) return false;
-    return a.localSizeBytes > REG_SPILL_MAX;
+    for (reg_kernel_t f : {r.fn, r.fn_rec}) {
+        hipFuncAttributes a;
+        if (hipFuncGetAttributes(&a, (const void*)f) != hipSuccess) continue;
+        if (a.localSizeBytes > REG_SPILL_MAX) return true;
+    }
+    return false;
 }
 
 static bool build_plan(int L, int n, int m, const int32_t* row_ptr, const int32_t* col_idx,

@@ -158,8 +158,21 @@ def _x_of_lam(bp, sl, lin, rho, xbar, lam):
     return bp[..., 0] + np.clip(a - bp[..., :-1], 0.0, np.diff(bp, axis=-1)).sum(-1)
 
 
-def prox(bp, sl, f0, W, xbar, rho, total, iters=200):
-    """Exact PH subproblem for all scenarios: (x [S, K], augmented objective [S])."""
+def prox(bp, sl, f0, W, xbar, rho, total, iters=200, method="auto"):
+    """Exact PH subproblem for all scenarios: (x [S, K], augmented objective [S]).
+
+    ``method="breakpoints"`` finds the acreage multiplier exactly: sum_k x_k(lam)
+    is piecewise linear and nonincreasing in lam, with kinks where a segment term of
+    ``_x_of_lam`` enters or leaves its clip range (lam = rho (xbar - b) - s - W for every
+    segment end b); it is evaluated at every kink >= 0 and interpolated linearly on the
+    piece that crosses the acreage ``total``.  ``method="bisect"`` bisects lam (``iters``
+    halvings); the two agree to rounding (tests/test_oracle_scale.py).  ``"auto"`` takes
+    the kinks for few crops (cm = 1: 6x faster) and bisection for many (the kink table
+    grows as K^2 per scenario)."""
+    if method == "auto":
+        method = "breakpoints" if sl.shape[1] <= 6 else "bisect"
+    if method == "breakpoints":
+        return _prox_breakpoints(bp, sl, f0, W, xbar, rho, total)
     S = bp.shape[0]
     lam = np.zeros(S)
     x = _x_of_lam(bp, sl, W, rho, xbar, lam)
@@ -179,6 +192,35 @@ def prox(bp, sl, f0, W, xbar, rho, total, iters=200):
             hi = np.where(gt, hi, mid)
         xh = _x_of_lam(bp, sl, W, rho, xbar, hi)
         x = np.where(over[:, None], xh, x)
+    obj = crop_cost(bp, sl, f0, x).sum(1) + (W * x).sum(1) + 0.5 * (rho * (x - xbar) ** 2).sum(1)
+    return x, obj
+
+
+def _prox_breakpoints(bp, sl, f0, W, xbar, rho, total, chunk_elems=1 << 24):
+    S, K, J = sl.shape
+    xbar = np.broadcast_to(xbar, W.shape)
+    rho = np.broadcast_to(rho, W.shape)
+    x = _x_of_lam(bp, sl, W, rho, xbar, np.zeros(S))
+    over = np.nonzero(x.sum(1) > total)[0]
+    P = 2 * K * J + 1
+    step = max(1, chunk_elems // (P * K * J))
+    for a in range(0, len(over), step):
+        ix = over[a:a + step]
+        b, s_, w, r, xb = bp[ix], sl[ix], W[ix], rho[ix], xbar[ix]
+        # kinks: lam where xbar - (s_i + W + lam) / rho equals b_{i-1} or b_i
+        base = (r * xb - w)[..., None] - s_                              # [n, K, J]
+        kinks = np.concatenate([base - r[..., None] * b[..., :-1], base - r[..., None] * b[..., 1:]], axis=2)
+        kinks = np.where(np.isfinite(kinks), kinks, 0.0).reshape(len(ix), -1)
+        lam = np.sort(np.concatenate([np.zeros((len(ix), 1)), np.maximum(kinks, 0.0)], axis=1), axis=1)
+        av = xb[:, None, :, None] - (s_[:, None] + (w[:, None, :] + lam[:, :, None])[..., None]) / r[:, None, :, None]
+        seg = np.clip(av - b[:, None, :, :-1], 0.0, np.diff(b, axis=-1)[:, None])
+        tot = (b[:, None, :, 0] + seg.sum(-1)).sum(-1)                    # [n, P], nonincreasing
+        j = np.argmax(tot <= total, axis=1)                               # first kink at or below
+        rows = np.arange(len(ix))
+        l1, l2 = lam[rows, j - 1], lam[rows, j]
+        t1, t2 = tot[rows, j - 1], tot[rows, j]
+        lam_star = l1 + (t1 - total) * (l2 - l1) / (t1 - t2)
+        x[ix] = _x_of_lam(b, s_, w, r, xb, lam_star)
     obj = crop_cost(bp, sl, f0, x).sum(1) + (W * x).sum(1) + 0.5 * (rho * (x - xbar) ** 2).sum(1)
     return x, obj
 

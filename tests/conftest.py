@@ -15,9 +15,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU test")
 
 
+def _gpu_selected(config):
+    """True when the run selects the GPU tests explicitly (``-m gpu`` or an expression
+    that requires the marker), as the round-end GPU tier does."""
+    expr = (config.getoption("-m", default="") or "").replace("(", " ").replace(")", " ").split()
+    return "gpu" in expr and "not" not in expr
+
+
 @pytest.fixture(scope="session")
-def gpu():
+def gpu(request):
+    """The MI355X. Under ``-m gpu`` a missing device FAILS the test: a GPU box whose torch
+    cannot see the card must not report a green GPU suite with nothing run.  Outside it
+    (a plain ``pytest tests`` on a CPU host) the GPU tests skip."""
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        msg = "no ROCm device visible (torch.cuda.is_available() is False)"
+        if _gpu_selected(request.config):
+            pytest.fail(msg + " under -m gpu", pytrace=False)
+        pytest.skip(msg)
     return torch.device("cuda:0")

@@ -1,6 +1,8 @@
 """Generate the configuration-scale farmer fixtures (tests/golden/farmer_scale.json).
 
 Run:  python tests/golden/make_golden_scale.py        (~1 minute, one core)
+      python tests/golden/make_golden_scale.py --conv (farmer_conv.json: config 3 run to
+                                                       convergence, ~30 minutes)
 
 Source: oracle/farmer_vec.py, the vectorised exact restatement of farmer.py:85-224 and
 PHBase.Iter0 / iterk_loop (phbase.py:758-979).  It is pinned by tests/test_oracle_scale.py:
@@ -68,7 +70,56 @@ def run(names, cm, iters, stride, num_scens=None):
     return out
 
 
+CONV_THRESH = (1e-2, 3e-3, 1e-3)
+
+
+def run_to_convergence(S=65536, limit=4000, stride=64):
+    """farmer_conv.json: config 3 (scen0..scen65535, cm=1, rho=1) run by iterk_loop until
+    conv < 1e-3 (phbase.py:925-934).  For every threshold of CONV_THRESH: the PH iteration
+    at which the loop breaks, and x̄ plus the W of every ``stride``-th scenario at that
+    iteration and its two neighbours (so a run that breaks one iteration off is compared
+    against its own iteration); the whole conv trajectory."""
+    t0 = time.time()
+    ph = FarmerVecPH([f"scen{i}" for i in range(S)], 1, rho=1.0)
+    tb = ph.iter0()
+    sample = list(range(0, S, stride))
+    conv, hit, kept, prev = [], {}, {thr: {} for thr in CONV_THRESH}, None
+    it = 0
+    while it < limit:
+        it += 1
+        xb = ph.compute_xbar()                                   # phbase.py:909
+        ph.W += ph.rho * (ph.x - ph.xbar)                        # :913
+        c = float(np.abs(ph.x - ph.xbar).sum() / (ph.S * ph.K))  # :916
+        conv.append(c)
+        snap = (xb.tolist(), ph.W[sample].tolist())
+        for thr in CONV_THRESH:
+            if thr in hit and it == hit[thr] + 1:
+                kept[thr][it] = snap
+            if thr not in hit and c < thr:
+                hit[thr] = it
+                kept[thr][it] = snap
+                if prev is not None:
+                    kept[thr][it - 1] = prev
+        prev = snap
+        if len(hit) == len(CONV_THRESH) and it > hit[CONV_THRESH[-1]]:
+            break
+        ph.x, ph.obj = fv.prox(ph.bp, ph.sl, ph.f0, ph.W, ph.xbar, ph.rho, ph.total)   # :941
+        if it % 100 == 0:
+            print(f"  iteration {it}: conv {c:.6g} ({time.time() - t0:.0f}s)", flush=True)
+    out = {"S": S, "crops_multiplier": 1, "rho": 1.0, "trivial_bound": tb, "sample": sample,
+           "conv": conv, "breaks": {}}
+    for thr in CONV_THRESH:
+        out["breaks"][repr(thr)] = {"iteration": hit[thr],
+                                    "xbar": {str(j): v[0] for j, v in sorted(kept[thr].items())},
+                                    "W": {str(j): v[1] for j, v in sorted(kept[thr].items())}}
+    print(f"{S} scen to conv < {CONV_THRESH[-1]}: breaks {hit} ({time.time() - t0:.0f}s)", flush=True)
+    with open(os.path.join(HERE, "farmer_conv.json"), "w") as f:
+        json.dump(out, f)
+
+
 def main():
+    if "--conv" in sys.argv:
+        return run_to_convergence()
     out = {}
     out["farmer65536_cm1"] = run([f"scen{i}" for i in range(65536)], 1, 5, 64)
     out["farmer1024_cm10"] = run([f"scen{i}" for i in range(1024)], 10, 0, 8)

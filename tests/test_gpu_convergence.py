@@ -1,0 +1,84 @@
+"""PH iterations to convergence at configuration scale (north_star: "the same PH iteration
+count to convergence +-1").
+
+Config 3 exactly as bench.py runs it -- farmer scen0..scen65535, cm = 1, rho = 1, the
+example's PH-solve options, the product loop PHBase.iterk_loop with its speculative
+solve -- run until conv < 1e-3 (phbase.py:925-934), against tests/golden/farmer_conv.json
+(make_golden_scale.py --conv: the exact vectorised oracle of oracle/farmer_vec.py, pinned
+in test_oracle_scale.py).  The reference loop breaks at PH iteration 1,078 for 1e-3 (331
+for 1e-2, 612 for 3e-3).
+
+Tolerances (north_star): iterations +-1; x̄ and W 1e-5 absolute at the iteration the GPU
+run stops (compared with the oracle's values at that same iteration); the conv
+trajectory within 1e-6 absolute at every iteration.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CONV = json.load(open(os.path.join(HERE, "golden", "farmer_conv.json")))
+ABS = 1e-5
+
+
+def _record_conv(ph):
+    """Wrap the engine's conv readbacks (both loop variants) to keep the trajectory."""
+    seen = []
+    e = ph.engine
+    wait, diff = e.convergence_wait, e.convergence_diff
+
+    def wait_rec():
+        v = wait()
+        seen.append(v)
+        return v
+
+    def diff_rec():
+        v = diff()
+        seen.append(v)
+        return v
+
+    e.convergence_wait, e.convergence_diff = wait_rec, diff_rec
+    return seen
+
+
+def test_config3_iterations_to_convergence(gpu):
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    S = CONV["S"]
+    names = farmer.scenario_names_creator(S)
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 1500, "defaultPHrho": 1.0, "convthresh": 1e-3,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": farmer.batch_creator,
+            "iterk_solver_options": dict(farmer.PDHG_ITERK_OPTIONS)}
+    ph = PH(opts, names, farmer.scenario_creator, scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": S})
+    ph.PH_Prep()
+    tb = ph.Iter0()
+    assert abs(tb - CONV["trivial_bound"]) <= 1e-5 * abs(CONV["trivial_bound"])
+    info = ph.engine.kernel_info()
+    assert info["lanes"] == 4 and (info["KC"], info["ZC"], info["KR"], info["ZR"]) == (3, 3, 2, 4), info
+    seen = _record_conv(ph)
+    ph.iterk_loop()
+    assert ph._speculate(False), "the bench's loop variant (speculative solve) must be the one tested"
+    assert ph.converged
+    k = ph._PHIter
+    want = CONV["breaks"]["0.001"]
+    assert abs(k - want["iteration"]) <= 1, (k, want["iteration"])
+    assert len(seen) == k
+    ref = np.array(CONV["conv"][:k])
+    dev = np.abs(np.array(seen) - ref)
+    assert dev.max() <= 1e-6, (dev.max(), int(dev.argmax()) + 1)
+    # the coarser thresholds along the same trajectory
+    for thr, key in ((1e-2, "0.01"), (3e-3, "0.003")):
+        first = int(np.argmax(np.array(seen) < thr)) + 1
+        assert abs(first - CONV["breaks"][key]["iteration"]) <= 1, (thr, first, CONV["breaks"][key]["iteration"])
+    # x̄ and W at the stopping iteration, against the oracle at that same iteration
+    xb = ph.xbar_by_node()["ROOT"][:3]
+    assert np.abs(xb - np.array(want["xbar"][str(k)])).max() <= ABS, (xb, want["xbar"][str(k)])
+    W = ph.W_array()[np.array(CONV["sample"])]
+    err = np.abs(W - np.array(want["W"][str(k)]))
+    assert err.max() <= ABS, (err.max(), CONV["sample"][int(err.max(1).argmax())])
+    assert (ph.engine.host("status") == 0).all()
