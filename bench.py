@@ -121,6 +121,39 @@ def _cpu_worker(args):
     return np.array(xs)
 
 
+def _cgroup_cpus():
+    """CPUs this process may use by its cgroup's CPU quota: (count or None, evidence).
+    cgroup v2 /sys/fs/cgroup/cpu.max ("QUOTA PERIOD" or "max PERIOD"), else v1
+    cpu.cfs_quota_us / cpu.cfs_period_us."""
+    try:
+        raw = open("/sys/fs/cgroup/cpu.max").read().strip()
+        q, per = raw.split()[:2]
+        return (None if q == "max" else max(1, int(int(q) // int(per)))), f"/sys/fs/cgroup/cpu.max = {raw!r}"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        ev = f"cpu.cfs_quota_us = {q}, cpu.cfs_period_us = {per}"
+        return (None if q <= 0 else max(1, q // per)), ev
+    except (OSError, ValueError):
+        return None, "no cgroup CPU quota file"
+
+
+def cpu_share():
+    """Worker count of the CPU baseline and its evidence: the cgroup quota when there is
+    one, capped by the affinity set; without a quota, the affinity set capped by
+    OMP_NUM_THREADS (which the GPU box sets to its per-GPU CPU share)."""
+    _, ncpu, aff = _host_cpu()
+    quota, ev = _cgroup_cpus()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if quota is not None:
+        return min(aff, quota), {"cgroup": ev, "cores_source": "cgroup CPU quota"}
+    if omp > 0:
+        return min(aff, omp), {"cgroup": ev, "cores_source": f"no quota; OMP_NUM_THREADS={omp} (the box's CPU share)"}
+    return aff, {"cgroup": ev, "cores_source": "no quota; sched_getaffinity"}
+
+
 def _host_cpu():
     model = None
     try:
@@ -145,8 +178,7 @@ def cpu_baseline(S_total, cm, rho, sample, iters=4):
     2..iters, scaled linearly to S_total scenarios."""
     import multiprocessing as mp
     model, ncpu, aff = _host_cpu()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    P = max(1, min(aff, share) if share > 0 else aff)
+    P, cores_ev = cpu_share()
     names = [f"scen{i}" for i in range(sample)]
     nn = 3 * cm
     avg = sample / P
@@ -172,10 +204,10 @@ def cpu_baseline(S_total, cm, rho, sample, iters=4):
             times.append(time.perf_counter() - t0)
     t_it = float(np.median(times[1:]))
     return {"value": 1.0 / (t_it * (S_total / sample)), "unit": "PH iterations/s", "cores": len(slices),
-            "kind": "port", "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "kind": "port", "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model, **cores_ev,
             "sample": (f"farmer cm={cm}: {sample} of {S_total} scenarios; Iter0 (HiGHS LP) + {iters} PH "
                        f"iterations (QPs by the oracle's dense IPM, one scenario at a time per worker, "
-                       f"{len(slices)} spawned workers = the process's CPU share); median per-iteration "
+                       f"{len(slices)} spawned workers, {cores_ev['cores_source']}); median per-iteration "
                        f"time of iterations 2..{iters} = {t_it:.3f}s, scaled x{S_total / sample:g} to "
                        f"{S_total} scenarios"),
             "sample_seconds_per_iteration": t_it, "wall_seconds": time.perf_counter() - t_start}
@@ -290,8 +322,8 @@ def uc_cpu_baseline(S_total, sample, rho_vec):
     per core of the process's CPU share."""
     import multiprocessing as mp
     model, ncpu, aff = _host_cpu()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    P = max(1, min(aff, share, sample) if share > 0 else min(aff, sample))
+    share, cores_ev = cpu_share()
+    P = max(1, min(share, sample))
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(P) as pool:
@@ -300,7 +332,7 @@ def uc_cpu_baseline(S_total, sample, rho_vec):
     per_scen = float(np.median([r for r in res]))
     t_it = per_scen * S_total / P
     return {"value": 1.0 / t_it, "unit": "PH iterations/s", "cores": P, "kind": "port",
-            "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model,
+            "host_cpus": ncpu, "affinity_cpus": aff, "cpu_model": model, **cores_ev,
             "sample": (f"uc: {sample} of {S_total} scenarios, one HiGHS dual-simplex LP each (the W-augmented "
                        f"PH subproblem without its prox term: no sparse QP solver here, so this is an upper "
                        f"bound on the CPU rate); median {per_scen:.2f}s per solve, {P} workers -> "
@@ -389,7 +421,6 @@ def main():
         opts["batch_creator"] = farmer.batch_creator
         ph = PH(opts, names, farmer.scenario_creator, mpicomm=comm,
                 scenario_creator_kwargs={"crops_multiplier": a.cm, "num_scens": a.scens})
-        tag = f"farmer{a.scens}_cm{a.cm}"
         workload = {(65536, 1): "farmer PH (config 3)",
                     (1024, 10): "farmer PH (config 2)"}.get((a.scens, a.cm), f"farmer PH, cm={a.cm}")
     elif a.model == "uc":
@@ -402,7 +433,6 @@ def main():
         rho_vec = uc.rho_vector(uc.scenario_creator(names[0], num_scens=a.scens))
         opts["rho_array"] = rho_vec
         ph = PH(opts, names, uc.scenario_creator, mpicomm=comm, scenario_creator_kwargs={"num_scens": a.scens})
-        tag = f"uc{a.scens}"
         workload = "UC LP relaxation PH (config 5)"
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             cpu = uc_cpu_baseline(a.scens, a.cpu_sample or 16, rho_vec)
@@ -417,13 +447,20 @@ def main():
         ph = PH(opts, names, aircond.scenario_creator, mpicomm=comm,
                 scenario_creator_kwargs={"branching_factors": a.bf, **AIRCOND_KW},
                 all_nodenames=create_nodenames_from_branching_factors(a.bf))
-        tag = f"aircond{a.scens}"
         workload = f"aircond multistage PH (config 4), bf {'x'.join(map(str, a.bf))}"
     with contextlib.redirect_stdout(sys.stderr):
         ph.PH_Prep()
         trivial_bound = ph.Iter0()
         e = ph.engine
         b = ph.batch
+        # Iter0's certification, summed over ranks: scenarios whose LP / QP stopped at the
+        # PDHG iteration cap (their x enters x̄ unconverged, the trivial bound is not a bound)
+        iter0_bad = torch.tensor([e.count_not_optimal()], dtype=torch.float64, device=e.device)
+        comm.allreduce_sum_(iter0_bad)
+        iter0_bad = int(iter0_bad.item())
+        # the PMC summaries under profiles/ are per GPU instance: keyed by the scenarios
+        # one rank holds (its kernel instance / lane count depend on it)
+        tag = {"farmer": f"farmer{b.S}_cm{a.cm}", "uc": f"uc{b.S}", "aircond": f"aircond{b.S}"}[a.model]
         ph.iterk_loop()                                # W warmup iterations (untimed)
         torch.cuda.synchronize()
         t_setup = time.perf_counter() - t_setup
@@ -438,6 +475,10 @@ def main():
         elapsed = time.perf_counter() - t0
     launches = e.instrumented()
     assert len(launches) == a.steps, (len(launches), a.steps)
+    bad_timed = torch.tensor(e.instrumented_not_optimal(), dtype=torch.float64, device=e.device)
+    comm.allreduce_sum_(bad_timed)
+    ar_ms = torch.tensor([e.instrumented_allreduce_ms() / a.steps], dtype=torch.float64, device=e.device)
+    comm.allreduce_max_(ar_ms)
     it_host = e.iters.cpu().numpy()
     t = torch.tensor([elapsed], dtype=torch.float64, device=e.device)
     comm.allreduce_max_(t)
@@ -479,10 +520,17 @@ def main():
             "solves_per_sec": ph_its * a.scens,
             "pdhg_iters_per_ph_iter": {"max": int(it_host.max()), "mean": float(it_host.mean())},
             "time_split_ms": {"solve_launch": rl["launch_ms"],
-                              "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"]},
+                              "allreduce": float(ar_ms.item()),
+                              "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"] - float(ar_ms.item())},
             "timed_region": "PHBase.iterk_loop (x̄, W, conv readback, solve_loop with gripe)",
-            "all_optimal": bool(n_bad.item() == 0),
-            "trivial_bound": trivial_bound,
+            # every timed solve: scenarios not OPTIMAL (summed over ranks), and the last one
+            "not_optimal_per_timed_solve_max": int(bad_timed.max().item()),
+            "all_optimal": bool(n_bad.item() == 0 and bad_timed.max().item() == 0),
+            "iter0_not_optimal": iter0_bad,
+            "trivial_bound_certified": iter0_bad == 0,
+            # an Iter0 that stopped at the iteration cap gives no certified bound
+            "trivial_bound": trivial_bound if iter0_bad == 0 else None,
+            "trivial_bound_uncertified": None if iter0_bad == 0 else trivial_bound,
             "setup_s": t_setup,
             "roofline": rl,
             "cpu_baseline": cpu,

@@ -160,6 +160,23 @@ int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double
                 double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
                 void* stream);
 
+/* Speculative solves.  PHBase.iterk_loop (phbase.py:909-957) decides after x̄ / W /
+ * conv whether the next solve_loop runs; the engine launches it before that decision
+ * and keeps it only if the loop goes on.  phgpu_solve_deferred is phgpu_solve except
+ * that the warm-start state it leaves (the iterate the next warm solve starts from,
+ * the primal weight, the work-queue predictor) goes to a second slot, which becomes the
+ * handle's state only at phgpu_commit; any other solve before that drops it, so a
+ * discarded speculative solve leaves the handle exactly as the last committed solve
+ * did.  Its outputs (x, y, obj, bound, status, iters) are written as by phgpu_solve.
+ * A PHGPU_SHARED_MATRIX handle (path 4) has one slot and rejects deferred solves. */
+int phgpu_solve_deferred(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
+                         double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
+                         void* stream);
+
+/* Make the warm-start state of the last phgpu_solve_deferred current (no-op if there is
+ * none pending).  Host-side bookkeeping only: no device work, no synchronisation. */
+int phgpu_commit(phgpu_handle h);
+
 /* Local x̄ partial sums (phbase.py:54-79): node_buf[2*num_nodes*nlen_max] gets
  *   [g*nlen_max + o]                        sum_s prob_coeff * x
  *   [num_nodes*nlen_max + g*nlen_max + o]   sum_s prob_coeff * x^2

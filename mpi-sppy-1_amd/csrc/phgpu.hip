@@ -119,6 +119,22 @@ struct phgpu_state {
     const double *W, *rho, *xbar;
     int W_on, prox_on;
     int have_solution;
+    // Warm-start slots (include/phgpu.h phgpu_solve_deferred / phgpu_commit).  The warm
+    // state a solve starts from -- the iterate x / y ([k][S] arrays or the records' x^ / y^
+    // fields), the primal weight omega and the queue predictor sk_iters -- lives in slot
+    // wslot; the fields above (x, y, omega, sk_iters, pk_X, pk_Y, have_solution, warm_rec)
+    // are bound to it at the start of every solve.  A solve writes its warm state to the
+    // *_w targets below: the same slot, or the other one for a deferred (speculative)
+    // solve, which becomes current only at phgpu_commit.
+    double *xs[2], *ys[2], *oms[2];
+    int32_t* its_s[2];
+    int pkXs[2], pkYs[2];
+    int have_s[2], warm_rec_s[2];
+    int wslot, wq;       // read slot / write slot of the current solve
+    int pending;         // slot of an uncommitted deferred solve, -1 none
+    double *xw, *yw, *omega_w;
+    int32_t* its_w;
+    int pk_XW, pk_YW;
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -555,13 +571,15 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     const int32_t* __restrict__ row_idx = st.row_idx;
     const double* __restrict__ Ahr = st.Ah_csr;
     const double* __restrict__ Ahc = st.Ah_csc;
-    double* __restrict__ x = st.x;
+    // the iterate lives in the write slot (the read slot for an ordinary solve); the
+    // warm start is read from st.x / st.y
+    double* __restrict__ x = st.xw;
     double* __restrict__ x0 = st.x0;
     double* __restrict__ xe = st.xe;
     double* __restrict__ xt = st.xt;
     double* __restrict__ aty = st.aty;
     double* __restrict__ aty0 = st.aty0;
-    double* __restrict__ y = st.y;
+    double* __restrict__ y = st.yw;
     double* __restrict__ y0 = st.y0;
     double* __restrict__ yt = st.yt;
     const double* __restrict__ ch = st.ch;
@@ -597,13 +615,13 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 
     // ---- start point
     for (int j = 0; j < n; ++j) {
-        double v = P.warm ? x[IX(j)] : 0.0;
+        double v = P.warm ? st.x[IX(j)] : 0.0;
         v = clampd(v, st.lbh[IX(j)], st.ubh[IX(j)]);
         x[IX(j)] = v;
         x0[IX(j)] = v;
     }
     for (int i = 0; i < m; ++i) {
-        const double v = P.warm ? y[IX(i)] : 0.0;
+        const double v = P.warm ? st.y[IX(i)] : 0.0;
         y[IX(i)] = v;
         y0[IX(i)] = v;
     }
@@ -810,7 +828,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     for (int j = 0; j < n; ++j) xout[IX(j)] = st.Dc[IX(j)] * x[IX(j)];
     if (yout)
         for (int i = 0; i < m; ++i) yout[IX(i)] = st.Dr[IX(i)] * y[IX(i)];
-    st.omega[s] = omega;
+    st.omega_w[s] = omega;
     obj[s] = pobj;
     bound[s] = dobj;
     status[s] = stat;
@@ -1290,8 +1308,29 @@ static hipError_t from_records(phgpu_state* h, int off, int moff, int K, double*
     return hipGetLastError();
 }
 
+// Point the warm-state fields at slot wslot (read) and slot ``wq`` (write; == wslot except
+// during a deferred solve) -- see the slot fields of phgpu_state.
+static void bind_slots(phgpu_state* h) {
+    const int p = h->wslot, wq = h->wq;
+    h->x = h->xs[p];
+    h->y = h->ys[p];
+    h->omega = h->oms[p];
+    h->sk_iters = h->its_s[p];
+    h->pk_X = h->pkXs[p];
+    h->pk_Y = h->pkYs[p];
+    h->have_solution = h->have_s[p];
+    h->warm_rec = h->warm_rec_s[p];
+    h->xw = h->xs[wq];
+    h->yw = h->ys[wq];
+    h->omega_w = h->oms[wq];
+    h->its_w = h->its_s[wq];
+    h->pk_XW = h->pkXs[wq];
+    h->pk_YW = h->pkYs[wq];
+}
+
 // record layout: A (CSR order) | c q Dc lb^ ub^ (n) | rl ru Dr rl^ ru^ (m) | x^ (n) y^ (m)
-// warm start | W rho xbar (nn) PH state of the current solve; stride rounded to 16 doubles
+// warm start of slot 0 | W rho xbar (nn) PH state of the current solve | x^ (n) y^ (m) warm
+// start of slot 1; stride rounded to 16 doubles
 static int pack_alloc(phgpu_state* h) {
     if (h->pk) return 0;
     const int n = h->n, m = h->m, nnz = h->nnz, nn = h->nn;
@@ -1312,7 +1351,12 @@ static int pack_alloc(phgpu_state* h) {
     h->pk_W = o; o += nn;
     h->pk_RHO = o; o += nn;
     h->pk_XB = o; o += nn;
+    h->pkXs[0] = h->pk_X;
+    h->pkYs[0] = h->pk_Y;
+    h->pkXs[1] = o; o += n;
+    h->pkYs[1] = o; o += m;
     h->pk_stride = (o + 15) / 16 * 16;
+    bind_slots(h);
     return dalloc(h, &h->pk, (size_t)h->pk_stride * (size_t)h->S);
 }
 
@@ -1592,6 +1636,24 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         ALLOC(h->yt, (size_t)m * Sz);
     }
     ALLOC(h->qhead, 1);
+    // warm-start slots: slot 0 is the arrays above; slot 1 (deferred solves, paths 1-3)
+    h->xs[0] = h->x;
+    h->ys[0] = h->y;
+    h->oms[0] = h->omega;
+    h->its_s[0] = h->sk_iters;
+    if (h->shared) {  // path 4 solves are never deferred: both slots are slot 0
+        h->xs[1] = h->x;
+        h->ys[1] = h->y;
+        h->oms[1] = h->omega;
+        h->its_s[1] = h->sk_iters;
+    } else {
+        ALLOC(h->xs[1], (size_t)n * Sz);
+        ALLOC(h->ys[1], (size_t)m * Sz);
+        ALLOC(h->oms[1], Sz);
+        ALLOC(h->its_s[1], Sz);
+    }
+    h->pending = -1;
+    bind_slots(h);
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
@@ -1876,10 +1938,13 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
     hipLaunchKernelGGL(k_sh_normbase, dim3(1), dim3(256), 0, st, *h, c, rl, ru);
     hipLaunchKernelGGL(k_sh_fill_omega, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
     HIPCHK(hipGetLastError());
-    h->have_solution = 0;
+    h->wslot = h->wq = 0;
+    h->pending = -1;
+    h->have_s[0] = h->have_s[1] = 0;
+    h->warm_rec_s[0] = h->warm_rec_s[1] = 0;
+    bind_slots(h);
     h->scen_set = 1;
     h->last_path = 0;
-    h->warm_rec = 0;
     return 0;
 }
 
@@ -1911,12 +1976,17 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     HIPCHK(cp(h->prob, prob, Sz));
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    h->wslot = h->wq = 0;
+    h->pending = -1;
+    h->have_s[0] = h->have_s[1] = 0;
+    h->warm_rec_s[0] = h->warm_rec_s[1] = 0;
+    bind_slots(h);
     HIPCHK(run_setup(h, st));
+    // the setup's start omega (slot 0) for slot 1 too
+    HIPCHK(hipMemcpyAsync(h->oms[1], h->oms[0], (size_t)h->S * sizeof(double), hipMemcpyDeviceToDevice, st));
     if (h->pk) HIPCHK(pack_fill(h, st));
-    h->have_solution = 0;
     h->scen_set = 1;
     h->last_path = 0;
-    h->warm_rec = 0;
     return 0;
 }
 
@@ -1933,11 +2003,43 @@ extern "C" int phgpu_set_ph_state(phgpu_handle h, const double* W, const double*
     return 0;
 }
 
+static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
+                      double* obj, double* bound, int32_t* status, int32_t* iters, void* stream);
+
 extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
                            double* y, double* obj, double* bound, int32_t* status,
                            int32_t* iters, void* stream) {
+    return solve_impl(h, opt, warm_start, 0, x, y, obj, bound, status, iters, stream);
+}
+
+extern "C" int phgpu_solve_deferred(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
+                                    double* y, double* obj, double* bound, int32_t* status,
+                                    int32_t* iters, void* stream) {
+    return solve_impl(h, opt, warm_start, 1, x, y, obj, bound, status, iters, stream);
+}
+
+extern "C" int phgpu_commit(phgpu_handle h) {
+    if (!h) return set_err(-1, "null handle");
+    if (h->pending >= 0) {
+        h->wslot = h->wq = h->pending;
+        h->pending = -1;
+        bind_slots(h);
+    }
+    return 0;
+}
+
+static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
+                      double* obj, double* bound, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return set_err(-1, "null handle");
     if (!x || !obj || !bound || !status) return set_err(-1, "null output pointer");
+    if (defer && h->shared)
+        return set_err(-1, "phgpu_solve_deferred: a shared-matrix handle (path 4) keeps one warm-start slot");
+    // read the committed slot; write it in place, or the other slot for a deferred solve
+    // (an uncommitted deferred solve is dropped by this one)
+    h->pending = -1;
+    h->wq = defer ? 1 - h->wslot : h->wslot;
+    bind_slots(h);
+    const int wq = h->wq;
     phgpu_options o;
     if (opt) o = *opt;
     else phgpu_default_options(&o);
@@ -2000,8 +2102,9 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters);
         HIPCHK(hipGetLastError());
-        h->have_solution = 1;
+        h->have_s[wq] = 1;
         h->last_path = 4;
+        bind_slots(h);
         return 0;
     }
     if (o.kernel == 2 && h->reg_inst < 0)
@@ -2012,6 +2115,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         return set_err(-1, "register-resident kernels require gamma = 1 (got %g)", o.gamma);
     const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? h->default_kernel : 1);
     const bool use_reg = path == 2;
+    int out_rec = 0;  // the warm state this solve writes lives in the records
     if (path == 3 && !h->pk) {
         const int rc3 = pack_alloc(h);
         if (rc3) return rc3;
@@ -2054,9 +2158,9 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
                            status, iters);
         HIPCHK(hipGetLastError());
         // outputs in the caller's scenario-fastest layout, unscaled
-        HIPCHK(from_records(h, h->pk_X, h->pk_DC, h->n, x, st));
-        if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
-        h->warm_rec = 1;
+        HIPCHK(from_records(h, h->pk_XW, h->pk_DC, h->n, x, st));
+        if (y) HIPCHK(from_records(h, h->pk_YW, h->pk_DR, h->m, y, st));
+        out_rec = 1;
     } else if (use_reg) {
         const int G = WAVE / h->reg_L;
         const reg_instance& ri = g_reg_instances[h->reg_inst];
@@ -2124,6 +2228,7 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         pl.row_c = h->pl_row_c;
         pl.order = h->sk_order;
         pl.last_iters = h->sk_iters;
+        pl.last_iters_w = h->its_w;
         pl.ema = h->have_solution ? 1 : 0;
         if (!rec) HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));  // record mode: k_reg_order did
         hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(WAVE * REG_WPB), lds, st, *h, P, pl, h->qhead, first_dyn,
@@ -2131,10 +2236,10 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
         HIPCHK(hipGetLastError());
         if (rec) {
             // outputs in the caller's scenario-fastest layout, unscaled
-            HIPCHK(from_records(h, h->pk_X, h->pk_DC, h->n, x, st));
-            if (y) HIPCHK(from_records(h, h->pk_Y, h->pk_DR, h->m, y, st));
+            HIPCHK(from_records(h, h->pk_XW, h->pk_DC, h->n, x, st));
+            if (y) HIPCHK(from_records(h, h->pk_YW, h->pk_DR, h->m, y, st));
         }
-        h->warm_rec = rec ? 1 : 0;
+        out_rec = rec ? 1 : 0;
         h->last_rec = rec ? 1 : 0;
     } else {
         if (P.warm && h->warm_rec) {
@@ -2142,11 +2247,17 @@ extern "C" int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_st
             HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
         }
         hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
-        h->warm_rec = 0;
+        out_rec = 0;
     }
     HIPCHK(hipGetLastError());
-    h->have_solution = 1;
+    // the warm state written by this solve; current now, or at phgpu_commit if deferred
+    h->have_s[wq] = 1;
+    h->warm_rec_s[wq] = out_rec;
     h->last_path = path;
+    if (defer) h->pending = wq;
+    else h->wslot = wq;
+    h->wq = h->wslot;
+    bind_slots(h);
     return 0;
 }
 
@@ -2254,6 +2365,12 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
 
 extern "C" int phgpu_destroy(phgpu_handle h) {
     if (!h) return 0;
+    if (h->oms[0]) {  // the x / y / omega / sk_iters fields may be bound to slot 1: free by slot
+        h->x = h->xs[0];
+        h->y = h->ys[0];
+        h->omega = h->oms[0];
+        h->sk_iters = h->its_s[0];
+    }
     void* ptrs[] = {h->row_ptr, h->col_idx, h->col_ptr, h->row_idx, h->perm, h->row_of,
                     h->nonant_col, h->nonant_depth, h->nonant_off, h->nonant_slot,
                     h->A, h->c, h->lb, h->ub, h->q, h->rl, h->ru, h->objc, h->prob, h->pcoef,
@@ -2268,6 +2385,11 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->sk_bins, h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (!h->shared) {  // warm-start slot 1 (slot 0 is x / y / omega / sk_iters above)
+        void* slot1[] = {h->xs[1], h->ys[1], h->oms[1], h->its_s[1]};
+        for (void* p : slot1)
+            if (p) (void)hipFree(p);
+    }
     delete h;
     return 0;
 }

@@ -44,7 +44,8 @@ SHARED_MATRIX = 1          # phgpu_create2 flag (include/phgpu.h)
 
 # every symbol include/phgpu.h declares (tests check the library exports them all)
 EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_scenarios", "phgpu_set_ph_state",
-           "phgpu_solve", "phgpu_ph_reduce", "phgpu_ph_update", "phgpu_expectations",
+           "phgpu_solve", "phgpu_solve_deferred", "phgpu_commit", "phgpu_ph_reduce", "phgpu_ph_update",
+           "phgpu_expectations",
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info"]
 
@@ -73,6 +74,8 @@ def load(path=None):
     lib.phgpu_set_ph_state.argtypes = [c_vp, c_vp, c_vp, c_vp, c_int, c_int]
     lib.phgpu_solve.argtypes = [c_vp, ctypes.POINTER(PhgpuOptions), c_int, c_vp, c_vp, c_vp, c_vp,
                                 c_vp, c_vp, c_vp]
+    lib.phgpu_solve_deferred.argtypes = lib.phgpu_solve.argtypes
+    lib.phgpu_commit.argtypes = [c_vp]
     lib.phgpu_ph_reduce.argtypes = [c_vp, c_vp, c_vp, c_vp]
     lib.phgpu_ph_update.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]
     lib.phgpu_expectations.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]

@@ -177,7 +177,11 @@ def drop_duplicate_rows(row_ptr, col_idx, A_val, rl, ru):
     declares its production-cost row once per piecewise segment
     (ReferenceModel_OK.py:1466-1470: indexed by (g, t, i), the body does not use i),
     which would otherwise add ~15k redundant rows and ~40% of the nonzeros.  Returns
-    the reduced arrays and the kept-row mask."""
+    the reduced arrays and the kept-row mask.
+
+    Candidates are found on the first scenario only (a dict keyed by its row bytes, so
+    no copy of the S-scenario arrays is held), and a candidate is dropped only after its
+    coefficients and range compare equal to the earlier row's in every scenario."""
     m = rl.shape[1]
     keep = np.ones(m, dtype=bool)
     seen = {}
@@ -185,11 +189,16 @@ def drop_duplicate_rows(row_ptr, col_idx, A_val, rl, ru):
         a, b = row_ptr[r], row_ptr[r + 1]
         if b == a:
             continue
-        key = (col_idx[a:b].tobytes(), A_val[:, a:b].tobytes(), rl[:, r].tobytes(), ru[:, r].tobytes())
-        if key in seen:
-            keep[r] = False
+        key = (col_idx[a:b].tobytes(), A_val[0, a:b].tobytes(), rl[0, r].tobytes(), ru[0, r].tobytes())
+        first = seen.setdefault(key, [])
+        for r0 in first:
+            a0 = row_ptr[r0]
+            if (np.array_equal(A_val[:, a:b], A_val[:, a0:a0 + (b - a)]) and np.array_equal(rl[:, r], rl[:, r0])
+                    and np.array_equal(ru[:, r], ru[:, r0])):
+                keep[r] = False
+                break
         else:
-            seen[key] = r
+            first.append(r)
     if keep.all():
         return row_ptr, col_idx, A_val, rl, ru, keep
     counts = np.diff(row_ptr)

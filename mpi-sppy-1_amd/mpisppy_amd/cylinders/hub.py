@@ -249,8 +249,13 @@ class Hub(SPCommunicator):
     # hub.py:163-172
     def hub_finalize(self):
         if self.layout is not None:
-            # the spokes' last bounds arrived with their final Gets (send_terminate)
-            pass
+            # the spokes' bounds after their finalize (the Lagrangian's final pass with
+            # the final W): the reference's hub_finalize runs after the spokes' finalize
+            # and a Barrier (spin_the_wheel.py:126-139)
+            for idx in sorted(self.ports):
+                bound, wid = self.ports[idx].final()
+                if wid > self._remote.get(idx, (math.nan, 0))[1]:
+                    self._remote[idx] = (bound, wid)
         if self.has_outerbound_spokes:
             self.receive_outerbounds()
         if self.has_innerbound_spokes:

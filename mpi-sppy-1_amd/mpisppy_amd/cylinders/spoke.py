@@ -66,10 +66,22 @@ class Spoke(SPCommunicator):
 
     # spoke.py:186-214 (the spoke's own loop when it has ranks of its own): prepare, then
     # alternate a Get of the hub's window with one pass of the loop body until the kill
-    # signal; ``port`` is a transport.SpokePort
+    # signal; ``port`` is a transport.SpokePort.  After finalize the final bound goes to
+    # the hub (its hub_finalize waits for it, as the reference's Barrier makes the hub wait
+    # for the spokes' finalize, spin_the_wheel.py:126-139); if anything raises, the hub is
+    # told instead of being left waiting.
     def run_remote(self, port):
-        from . import transport as tp
         self._remote = True
+        try:
+            result = self._run_remote(port)
+        except BaseException:
+            port.post_failure()
+            raise
+        port.post_final(getattr(self, "_bound", float("nan")), self.local_write_id)
+        return result
+
+    def _run_remote(self, port):
+        from . import transport as tp
         self.main()
         nn, S = max(self.opt.batch.nn, 1), self.opt.batch.S
         device = self.opt.engine.device if self.opt.engine is not None else None

@@ -26,7 +26,16 @@ in pull mode:
 
 The hub never waits for a spoke inside the PH loop (a check costs ~25 us, a 196 KB
 window ~85 us on one node), and a spoke always receives the hub's current values.
+
+Termination (spin_the_wheel.py:126-139 runs the spokes' finalize, a Barrier, then
+hub_finalize, so a spoke's last bound -- the Lagrangian's final pass with the final W --
+counts): after its finalize a spoke sets one more key, ``fin``, holding its final bound
+and write id, and the hub's ``hub_finalize`` waits for it before the last bound update.
+A spoke whose loop raises sets its request / ``fin`` keys with the failure flag, and
+every hub wait has a time limit (``timeout``); either ends the hub with an error that
+names the spoke's cylinder instead of a hang.
 """
+import datetime
 import itertools
 import struct
 
@@ -37,7 +46,13 @@ import torch.distributed as dist
 from ..comm import Comm
 
 KILL = -1.0
-_REQ = struct.Struct("<4d")   # [bound, bound write id, last hub write id seen, spare]
+FAILED = 1.0
+_REQ = struct.Struct("<4d")   # [bound, bound write id, last hub write id seen, failure flag]
+WAIT_TIMEOUT = datetime.timedelta(seconds=1800)   # longest a hub waits on one spoke key
+
+
+class SpokeFailure(RuntimeError):
+    """A spoke on its own ranks stopped with an error, or never answered in time."""
 _serial = itertools.count()   # one key prefix per wheel (every rank creates layouts in order)
 
 
@@ -104,45 +119,82 @@ class StrataComm:
 class HubPort:
     """Hub side of one spoke's window pair (this hub rank <-> its strata peer)."""
 
-    def __init__(self, layout, spoke_cylinder, payload_len):
+    def __init__(self, layout, spoke_cylinder, payload_len, timeout=WAIT_TIMEOUT):
         self.store = layout.store
+        self.spoke = spoke_cylinder
+        self.rank = layout.cyl_rank
         self.req_key = f"{layout.prefix}req/{spoke_cylinder}/{layout.cyl_rank}"
         self.win_key = f"{layout.prefix}win/{spoke_cylinder}/{layout.cyl_rank}"
+        self.fin_key = f"{layout.prefix}fin/{spoke_cylinder}/{layout.cyl_rank}"
         self.n = payload_len
         self.buf = np.empty(payload_len + 3)
+        self.timeout = timeout
 
     def ready(self):
         return self.store.check([self.req_key])
 
+    def _take(self, key, what):
+        try:
+            self.store.wait([key], self.timeout)
+        except Exception as e:  # the store raises on its deadline
+            raise SpokeFailure(f"spoke cylinder {self.spoke} (rank {self.rank} of its cylinder) did not post "
+                               f"its {what} within {self.timeout}: {e}") from e
+        bound, bound_wid, _, failed = _REQ.unpack(self.store.get(key))
+        self.store.delete_key(key)
+        if failed == FAILED:
+            raise SpokeFailure(f"spoke cylinder {self.spoke} (rank {self.rank} of its cylinder) stopped with an "
+                               f"error (see that rank's output)")
+        return bound, bound_wid
+
     def answer(self, values, outer, inner, write_id):
-        """Take the waiting request (blocks until there is one) and set the window;
-        returns the (bound, bound write id) that came with the request."""
-        self.store.wait([self.req_key])
-        bound, bound_wid, _, _ = _REQ.unpack(self.store.get(self.req_key))
-        self.store.delete_key(self.req_key)
+        """Take the waiting request (blocks until there is one, at most ``timeout``) and
+        set the window; returns the (bound, bound write id) that came with the request."""
+        bound, bound_wid = self._take(self.req_key, "request")
         if values is not None:
             self.buf[:self.n] = values.numpy().reshape(-1)[:self.n]
         self.buf[self.n:] = (outer, inner, write_id)
         self.store.set(self.win_key, self.buf.tobytes())
         return bound, bound_wid
 
+    def final(self):
+        """The spoke's bound after its finalize (spoke.py finalize -> spin_the_wheel.py:132
+        Barrier -> hub_finalize): (bound, bound write id)."""
+        return self._take(self.fin_key, "final bound")
+
 
 class SpokePort:
     """Spoke side: one Get = request + wait for the hub's answer."""
 
-    def __init__(self, layout, payload_len):
+    def __init__(self, layout, payload_len, timeout=WAIT_TIMEOUT):
         self.store = layout.store
         self.req_key = f"{layout.prefix}req/{layout.cylinder}/{layout.cyl_rank}"
         self.win_key = f"{layout.prefix}win/{layout.cylinder}/{layout.cyl_rank}"
+        self.fin_key = f"{layout.prefix}fin/{layout.cylinder}/{layout.cyl_rank}"
         self.n = payload_len
+        self.timeout = timeout
+        self.requested = False   # a request is posted and not yet answered
 
     def get(self, bound, bound_wid, seen_wid):
         self.store.set(self.req_key, _REQ.pack(float(bound), float(bound_wid), float(seen_wid), 0.0))
-        self.store.wait([self.win_key])
+        self.requested = True
+        self.store.wait([self.win_key], self.timeout)
+        self.requested = False
         buf = np.frombuffer(self.store.get(self.win_key), dtype=np.float64)
         self.store.delete_key(self.win_key)
         vals = torch.from_numpy(buf[:self.n].copy())
         return vals, float(buf[self.n]), float(buf[self.n + 1]), float(buf[self.n + 2])
+
+    def post_final(self, bound, bound_wid):
+        """The bound after finalize, for the hub's hub_finalize."""
+        self.store.set(self.fin_key, _REQ.pack(float(bound), float(bound_wid), 0.0, 0.0))
+
+    def post_failure(self):
+        """Tell the hub this spoke has stopped: whichever key it waits on next -- a
+        request (unless one is already posted) or the final bound -- carries the flag."""
+        msg = _REQ.pack(float("nan"), 0.0, 0.0, FAILED)
+        if not self.requested:
+            self.store.set(self.req_key, msg)
+        self.store.set(self.fin_key, msg)
 
 
 def ci_order(t_nn_S):

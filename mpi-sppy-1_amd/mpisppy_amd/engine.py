@@ -194,7 +194,9 @@ class PHEngine:
         iteration counts (one D2D copy after the launch, outside the event pair).  Used
         by bench.py for the per-launch roofline inside its timed region."""
         self._ins = {"events": [], "iters": torch.empty((max_solves, self.S), dtype=torch.int32,
-                                                         device=self.device)}
+                                                         device=self.device),
+                     "not_optimal": torch.zeros(max_solves, dtype=torch.int64, device=self.device),
+                     "ar_events": []}
 
     def instrumented(self):
         """[(launch ms, scenario-iterations)] of the recorded launches (syncs)."""
@@ -206,14 +208,44 @@ class PHEngine:
         its = ins["iters"][:k].sum(dim=1, dtype=torch.int64).cpu().tolist()
         return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
 
+    def instrumented_not_optimal(self):
+        """Scenarios not OPTIMAL in each recorded launch."""
+        ins = getattr(self, "_ins", None)
+        if not ins:
+            return []
+        return ins["not_optimal"][:len(ins["events"])].cpu().tolist()
+
+    def instrumented_allreduce_ms(self):
+        """Total ms of the x̄ / conv all-reduces issued while instrumenting (HIP events on
+        the current stream around each collective; 0 with one rank, where they are no-ops)."""
+        ins = getattr(self, "_ins", None)
+        if not ins:
+            return 0.0
+        torch.cuda.synchronize(self.device)
+        return float(sum(a.elapsed_time(b) for a, b in ins["ar_events"]))
+
+    def _allreduce_sum_(self, t):
+        """comm.allreduce_sum_ with HIP events around it while instrumenting."""
+        ins = getattr(self, "_ins", None)
+        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["iters"].shape[0]:
+            return self.comm.allreduce_sum_(t)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        self.comm.allreduce_sum_(t)
+        ev[1].record()
+        ins["ar_events"].append(ev)
+        return t
+
     # -------------------------------------------------------------- hot path
     _OUTS = ("x", "y", "obj", "bound", "status", "iters")
 
     def solve(self, options=None, warm=True, speculative=False):
         """phgpu_solve into the output tensors (x, y, obj, bound, status, iters), or with
-        ``speculative`` into a second set that ``commit()`` swaps in and any other call
-        leaves unused (PHBase.iterk_loop launches the next solve before it knows whether
-        the convergence test stops the loop)."""
+        ``speculative`` (phgpu_solve_deferred) into a second set that ``commit()`` swaps in
+        (PHBase.iterk_loop launches the next solve before it knows whether the convergence
+        test stops the loop).  An uncommitted speculative solve changes nothing: its
+        outputs stay in the spare set and the library keeps its warm-start state in a
+        second slot that only phgpu_commit makes current (include/phgpu.h)."""
         o = options if options is not None else _lib.default_options()
         if speculative:
             if not hasattr(self, "_spec"):
@@ -226,23 +258,26 @@ class PHEngine:
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        _lib.check(self.lib.phgpu_solve(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
-                                        _ptr(out["y"] if self.want_duals else None), _ptr(out["obj"]),
-                                        _ptr(out["bound"]),
-                                        _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
-                   "phgpu_solve")
+        fn = self.lib.phgpu_solve_deferred if speculative else self.lib.phgpu_solve
+        _lib.check(fn(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
+                      _ptr(out["y"] if self.want_duals else None), _ptr(out["obj"]), _ptr(out["bound"]),
+                      _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
+                   "phgpu_solve_deferred" if speculative else "phgpu_solve")
         if rec:
             ev[1].record()
-            ins["iters"][len(ins["events"])].copy_(out["iters"])
+            k = len(ins["events"])
+            ins["iters"][k].copy_(out["iters"])
+            ins["not_optimal"][k] = (out["status"] != 0).sum()
             ins["events"].append(ev)
             ins.setdefault("spec", []).append(speculative)
 
     def commit(self):
-        """Make the last speculative solve's outputs the current ones."""
+        """Make the last speculative solve's outputs and warm-start state the current ones."""
         for k in self._OUTS:
             cur = getattr(self, k)
             setattr(self, k, self._spec[k])
             self._spec[k] = cur
+        _lib.check(self.lib.phgpu_commit(self.h), "phgpu_commit")
 
     def _status_counts(self):
         if not hasattr(self, "_counts_dev"):
@@ -279,7 +314,7 @@ class PHEngine:
     def compute_xbar(self):
         """Local partials + cross-rank sum (phbase.py:27-87); result left in node_buf."""
         self.compute_xbar_partials()
-        combine_node_partials(self.comm, self.node_buf)
+        self._allreduce_sum_(self.node_buf)
         return self.node_buf
 
     def update(self, update_W=True):
@@ -290,7 +325,7 @@ class PHEngine:
 
     def convergence_diff(self):
         """phbase.py:330-343: sum over ranks of per-rank means, / n_proc (host float)."""
-        self.comm.allreduce_sum_(self.conv_buf)
+        self._allreduce_sum_(self.conv_buf)
         return float(self.conv_buf.item()) / self.comm.size
 
     def convergence_diff_async(self):
@@ -299,7 +334,7 @@ class PHEngine:
         if not hasattr(self, "_conv_host"):
             self._conv_host = torch.zeros(1, dtype=torch.float64).pin_memory()
             self._conv_ev = torch.cuda.Event()
-        self.comm.allreduce_sum_(self.conv_buf)
+        self._allreduce_sum_(self.conv_buf)
         self._conv_host.copy_(self.conv_buf, non_blocking=True)
         self._conv_ev.record()
 

@@ -87,6 +87,7 @@ def solve_qp_ipm(A, rl, ru, lb, ub, c, q, tol=1e-11, max_iter=200, polish=True):
     gnorm = 1.0 + np.abs(g).max(initial=0.0)
     rnorm = 1.0 + np.abs(r).max(initial=0.0)
     status = 1
+    mu_hist = []
     for it in range(max_iter):
         dl = np.where(fl, w - lw, 1.0)
         du = np.where(fu, uw - w, 1.0)
@@ -136,6 +137,12 @@ def solve_qp_ipm(A, rl, ru, lb, ub, c, q, tol=1e-11, max_iter=200, polish=True):
         mu_aff = (np.sum(((dl + ap * dw) * (zl + ad * dzl))[fl]) +
                   np.sum(((du - ap * dw) * (zu + ad * dzu))[fu])) / ncomp
         sigma = (mu_aff / max(mu, 1e-300)) ** 3
+        # safeguard: Mehrotra's corrector can cycle without reducing mu (seen on a few
+        # PH-augmented aircond QPs: a period-4 orbit at mu ~ 0.13); after 5 iterations
+        # without halving mu, take a well-centred step instead
+        mu_hist.append(mu)
+        if len(mu_hist) > 5 and mu > 0.5 * mu_hist[-6]:
+            sigma = max(sigma, 0.5)
         tl = np.where(fl, sigma * mu - dw * dzl, 0.0)
         tu = np.where(fu, sigma * mu + dw * dzu, 0.0)
         dw, dlam, dzl, dzu = newton(tl, tu)
@@ -188,6 +195,49 @@ def _polish(A, rl, ru, lb, ub, c, q, w, zl, zu, lw, uw, fl, fu, M, r, h, g, n):
 
 
 # ------------------------------------------------------- farmer closed form
+def kkt_certify(A, rl, ru, lb, ub, c, q, x, act_tol=1e-7):
+    """Certify that x solves  min c'x + 1/2 sum q x^2  s.t. rl <= Ax <= ru, lb <= x <= ub
+    (q >= 0, a convex QP) by its KKT conditions: x feasible, and multipliers with the
+    right signs on the active bounds / rows (y_i >= 0 on a row at rl, <= 0 at ru, free on
+    an equality; reduced costs >= 0 at lb, <= 0 at ub) that make q x + c - A'y - r = 0.
+    The multipliers come from a bounded least-squares fit (scipy lsq_linear); returns
+    (primal violation, stationarity residual), both relative to 1 + max|c|.  For the
+    oracle's IPM runs that stop short of its own tolerance: their polished x is accepted
+    when both are tiny (make_golden_aircond.py)."""
+    from scipy.optimize import lsq_linear
+    A = np.asarray(A, float)
+    m, n = A.shape
+    scale = 1.0 + np.abs(c).max(initial=0.0)
+    ax = A @ x
+    pviol = max(np.maximum(rl - ax, 0).max(initial=0), np.maximum(ax - ru, 0).max(initial=0),
+                np.maximum(lb - x, 0).max(initial=0), np.maximum(x - ub, 0).max(initial=0))
+    tol_r = act_tol * (1.0 + np.abs(ax))
+    tol_x = act_tol * (1.0 + np.abs(x))
+    at_rl = np.isfinite(rl) & (ax - rl <= tol_r)
+    at_ru = np.isfinite(ru) & (ru - ax <= tol_r)
+    at_lb = np.isfinite(lb) & (x - lb <= tol_x)
+    at_ub = np.isfinite(ub) & (ub - x <= tol_x)
+    cols, lo, hi = [], [], []
+    for i in range(m):                       # y_i: row multipliers
+        if at_rl[i] or at_ru[i]:
+            cols.append(A[i])
+            lo.append(0.0 if not at_ru[i] else -INF)
+            hi.append(0.0 if not at_rl[i] else INF)
+    for j in range(n):                       # reduced costs of active column bounds
+        if at_lb[j] or at_ub[j]:
+            e = np.zeros(n)
+            e[j] = 1.0
+            cols.append(e)
+            lo.append(0.0 if not at_ub[j] else -INF)
+            hi.append(0.0 if not at_lb[j] else INF)
+    grad = q * x + c
+    if not cols:
+        return pviol / scale, np.abs(grad).max() / scale
+    M = np.array(cols).T
+    sol = lsq_linear(M, grad, bounds=(np.array(lo), np.array(hi)), method="bvls", tol=1e-14)
+    return pviol / scale, np.abs(M @ sol.x - grad).max() / scale
+
+
 def _farmer_crop_pieces(base, Y, cm):
     """Convex piecewise-linear first+second stage cost of one crop as a function of its
     acreage x in [0, 500*cm]: returns (breakpoints, slopes, value at 0).

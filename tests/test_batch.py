@@ -78,3 +78,20 @@ def test_rank_slices_and_node_idx():
         avg = S / P
         assert all(x[0] == int(i * avg) for i, x in enumerate(sl))
     assert node_idx([], [4, 3, 2]) == 0 and node_idx([1], [4, 3, 2]) == 2 and node_idx([1, 2], [4, 3, 2]) == 10
+
+
+def test_drop_duplicate_rows_checks_every_scenario():
+    """A row is dropped only if an earlier row equals it in EVERY scenario (the UC
+    production-cost rows, ReferenceModel_OK.py:1466-1470); rows equal in scenario 0 only
+    are kept."""
+    from mpisppy_amd.batch import drop_duplicate_rows
+    row_ptr = np.array([0, 2, 4, 6, 8], dtype=np.int32)
+    col_idx = np.array([0, 1, 0, 1, 0, 1, 1, 2], dtype=np.int32)
+    A = np.array([[1.0, 2.0, 1.0, 2.0, 1.0, 2.0, 3.0, 4.0],
+                  [1.0, 2.0, 1.0, 2.0, 1.0, 5.0, 3.0, 4.0]])      # row 2 differs in scenario 1
+    rl = np.array([[0.0, 0.0, 0.0, -np.inf], [0.0, 0.0, 0.0, -np.inf]])
+    ru = np.array([[1.0, 1.0, 1.0, 2.0], [1.0, 1.0, 1.0, 2.0]])
+    rp, ci, Av, l, u, keep = drop_duplicate_rows(row_ptr, col_idx, A, rl, ru)
+    assert keep.tolist() == [True, False, True, True]
+    assert rp.tolist() == [0, 2, 4, 6] and ci.tolist() == [0, 1, 0, 1, 1, 2]
+    assert Av.shape == (2, 6) and l.shape == (2, 3) and u.shape == (2, 3)

@@ -1,0 +1,89 @@
+"""The speculative solve of PHBase.iterk_loop changes nothing the reference loop would not.
+
+iterk_loop launches iteration k+1's solve before the host reads conv (the solve depends
+only on W and x̄, final after Update_W), and keeps it only when the loop goes on
+(phbase.py:909-957 order: x̄ -> W -> conv -> break? -> solve).  The launch goes through
+phgpu_solve_deferred: its outputs land in a spare set and its warm-start state in the
+library's second slot, made current only by phgpu_commit.  So a run with the speculative
+solve and one without give bit-identical x̄, W, conv and iteration counts, and a solve
+after the convergence break warm-starts from the last committed iterate in both --
+checked here bit for bit on the register path in scenario order and in record mode, on
+the global-memory kernel, and on the multistage aircond tree.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _farmer(S, spec, thresh, kernel=0):
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    so = {"kernel": kernel} if kernel else {}
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 2000, "defaultPHrho": 1.0, "convthresh": thresh,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": farmer.batch_creator, "speculative_solve": spec,
+            "iter0_solver_options": dict(so), "iterk_solver_options": dict(so)}
+    return PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+              scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": S})
+
+
+def _aircond(spec, thresh):
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import aircond
+    from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+    bf = [4, 3, 2]
+    kw = {"branching_factors": bf, "Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50, "mu_dev": 0,
+          "sigma_dev": 40, "start_seed": 0}
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 2000, "defaultPHrho": 1.0, "convthresh": thresh,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": aircond.batch_creator, "speculative_solve": spec}
+    return PH(opts, aircond.scenario_names_creator(24), aircond.scenario_creator, scenario_creator_kwargs=kw,
+              all_nodenames=create_nodenames_from_branching_factors(bf))
+
+
+def _run(make, spec):
+    ph = make(spec)
+    ph.ph_main(finalize=False)
+    assert ph.converged
+    assert ph._speculate(False) == spec
+    e = ph.engine
+    out = {"iter": ph._PHIter, "conv": ph.conv, "W": e.W.cpu().numpy().copy(),
+           "xbar": e.xbar.cpu().numpy().copy(), "node_buf": e.node_buf.cpu().numpy().copy(),
+           "x": e.x.cpu().numpy().copy()}
+    # one more solve after the break: warm-started from the last committed solve
+    ph.solve_loop(solver_options=ph.iterk_solver_options, gripe=True)
+    out["x_after"] = e.x.cpu().numpy().copy()
+    out["iters_after"] = e.iters.cpu().numpy().copy()
+    out["kernel"] = e.kernel_info()
+    return out
+
+
+CASES = {
+    "farmer3": lambda spec: _farmer(3, spec, 1e-3),
+    "farmer4096_record_mode": lambda spec: _farmer(4096, spec, 3e-2),
+    "farmer256_global_kernel": lambda spec: _farmer(256, spec, 3e-2, kernel=1),
+    "aircond432": lambda spec: _aircond(spec, 1e-4),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_speculative_solve_is_invisible(gpu, case):
+    keep = os.environ.get("PHGPU_REG_REC")
+    if case == "farmer4096_record_mode":
+        os.environ["PHGPU_REG_REC"] = "1"
+    try:
+        a = _run(CASES[case], True)
+        b = _run(CASES[case], False)
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_REG_REC", None)
+        else:
+            os.environ["PHGPU_REG_REC"] = keep
+    if case == "farmer4096_record_mode":
+        assert a["kernel"]["rec"] == 1, a["kernel"]
+    assert a["iter"] == b["iter"] and a["conv"] == b["conv"], (a["iter"], b["iter"], a["conv"], b["conv"])
+    for k in ("W", "xbar", "node_buf", "x", "x_after", "iters_after"):
+        assert np.array_equal(a[k], b[k]), (case, k, np.abs(a[k] - b[k]).max())

@@ -109,3 +109,22 @@ def test_rank_slices_match_reference_formula():
     assert rank_slices(3, 1) == [[0, 1, 2]]
     assert rank_slices(10, 3) == [[0, 1, 2], [3, 4, 5], [6, 7, 8, 9]]
     assert extract_num("scen0012") == 12
+
+
+def test_ipm_does_not_cycle_on_ph_augmented_aircond_qp():
+    """A PH subproblem of config 4 (aircond scen5371, PH iteration 3) on which Mehrotra's
+    corrector cycled; with the centring safeguard the IPM converges, and lpqp.kkt_certify
+    confirms the answer independently (feasible, signed multipliers, stationarity)."""
+    import json
+    from oracle.lpqp import solve_qp_ipm, kkt_certify
+    g = json.load(open(os.path.join(HERE, "golden", "aircond_qp_cycling.json")))
+    f = lambda k: np.where(np.abs(np.array(g[k])) >= g["inf_as"], np.sign(g[k]) * np.inf, g[k])  # noqa: E731
+    A, rl, ru, lb, ub, c, q = (f(k) for k in ("A", "rl", "ru", "lb", "ub", "c", "q"))
+    x, obj, st = solve_qp_ipm(A, rl, ru, lb, ub, c, q)
+    assert st == 0
+    pv, sv = kkt_certify(A, rl, ru, lb, ub, c, q, x)
+    assert pv <= 1e-12 and sv <= 1e-12, (pv, sv)
+    xb = x.copy()
+    xb[0] += 1.0
+    xb[2] += 1.0                      # still feasible (material balance), not optimal
+    assert kkt_certify(A, rl, ru, lb, ub, c, q, xb)[1] > 1e-3

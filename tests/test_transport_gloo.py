@@ -56,6 +56,9 @@ def _worker(rank, world, port, out_dir, n_spokes):
             for k in sorted(ports):
                 b, wid = ports[k].answer(tp.ci_order(W), 0.0, 0.0, tp.KILL)
                 got.setdefault(k, []).append((13, b, wid))
+            for k in sorted(ports):          # hub_finalize: the bound after the spoke's finalize
+                b, wid = ports[k].final()
+                got.setdefault(k, []).append((14, b, wid))
             np.save(os.path.join(out_dir, f"hub{rank}.npy"),
                     np.array([(k, it, b, wid) for k, v in got.items() for (it, b, wid) in v]))
         else:
@@ -77,6 +80,7 @@ def _worker(rank, world, port, out_dir, n_spokes):
                 rows.append((it, lay.cylinder, lay.cyl_rank, 0))
                 time.sleep(0.025 * lay.cylinder)          # spokes work at different speeds
                 bound, bwid = 10.0 * it + lay.cylinder, bwid + 1
+            p.post_final(777.0 + lay.cylinder, bwid + 1)      # finalize's bound
             np.save(os.path.join(out_dir, f"spoke{rank}.npy"), np.array(rows))
         dist.barrier()
     finally:
@@ -94,6 +98,9 @@ def test_transport_windows(tmp_path, world, n_spokes):
         assert np.array_equal(h[:, :2], hubs[0][:, :2])
     for k in range(1, n_spokes + 1):
         ans = hubs[0][hubs[0][:, 0] == k]
+        fin = ans[-1]
+        ans = ans[:-1]
+        assert fin[1] == 14 and fin[2] == 777.0 + k and fin[3] > ans[-1][3]   # the final bound arrives
         its = ans[:, 1]
         assert its[-1] == 13 and np.all(np.diff(its) > 0) and len(its) >= 3
         # the bound that came back with each Get is the one computed from the previous
@@ -104,3 +111,47 @@ def test_transport_windows(tmp_path, world, n_spokes):
             sp = np.load(tmp_path / f"spoke{k * P + r}.npy")
             assert sp[-1][0] == -1
             assert list(sp[:-1, 0]) == list(its[:-1])
+
+
+def _failing_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "mpi-sppy-1_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mpisppy_amd.cylinders import transport as tp
+        lay = tp.CylinderLayout(2)
+        if lay.cylinder == 0:
+            hp = tp.HubPort(lay, 1, NN * S)
+            W = torch.zeros(NN, S, dtype=torch.float64)
+            hp.answer(tp.ci_order(W), 0.0, 0.0, 1.0)
+            msg = ""
+            while not hp.ready():
+                time.sleep(0.01)
+            try:
+                hp.answer(tp.ci_order(W), 0.0, 0.0, 2.0)
+            except tp.SpokeFailure as e:
+                msg = str(e)
+            with open(os.path.join(out_dir, "hub.txt"), "w") as f:
+                f.write(msg)
+        else:
+            p = tp.SpokePort(lay, NN * S)
+            p.get(float("nan"), 0, 0)
+            try:
+                raise ValueError("spoke loop body failed")      # e.g. in do_work
+            except ValueError:
+                p.post_failure()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_failed_spoke_is_reported_not_waited_for(tmp_path):
+    """A spoke that raises posts the failure flag (Spoke.run_remote); the hub's next wait
+    on it raises SpokeFailure naming the cylinder instead of hanging."""
+    mp.spawn(_failing_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    msg = (tmp_path / "hub.txt").read_text()
+    assert "spoke cylinder 1" in msg and "stopped with an error" in msg, msg

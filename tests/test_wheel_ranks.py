@@ -4,7 +4,8 @@ windows of cylinders/transport.py.  Ranks are gloo processes sharing cuda:0 (1 o
 cylinder).  The asynchronous schedule changes the bound trajectory, so the check is on
 what does not depend on it: the outer bound is valid (<= the EF optimum), the inner
 bound reaches the EF optimum (test_sc.py:30-38: x* = 80/250/170, obj -108390), the gap
-closes to rel_gap, and every rank learns the same final bounds.  The hub never waits for
+closes to rel_gap, every rank learns the same final bounds, and the Lagrangian's final
+bound (computed after the kill signal) is counted in the hub's.  The hub never waits for
 a spoke (as in the reference), so the iteration cap is set high enough that termination
 comes from the gap, however slowly the spokes run on the shared GPU."""
 import os
@@ -52,9 +53,10 @@ def _worker(rank, world, port, out_dir):
         ws = WheelSpinner(hub, spokes)
         ws.spin()
         it = ws.spcomm.opt._PHIter if ws.strata_rank == 0 else -1
+        fin = getattr(ws.spokes[0], "final_bound", None) if ws.strata_rank == 1 else None
         np.save(os.path.join(out_dir, f"r{rank}.npy"),
                 np.array([ws.BestInnerBound, ws.BestOuterBound, ws.strata_rank, ws.cylinder_rank, it,
-                          1.0 if ws.placement == "ranks" else 0.0]))
+                          1.0 if ws.placement == "ranks" else 0.0, np.nan if fin is None else fin]))
     finally:
         dist.destroy_process_group()
 
@@ -74,3 +76,8 @@ def test_wheel_on_separate_ranks(gpu, tmp_path, world):
     assert abs(ib - FARMER_EF_OBJ) <= 1e-4 * abs(FARMER_EF_OBJ), ib
     assert (ib - ob) / abs(ob) <= 1e-4 + 1e-9                     # terminated on rel_gap
     assert 1 <= r[0, 4] < 20000
+    # the Lagrangian's final pass (with the final W, after the kill signal) reaches the hub
+    # before hub_finalize, as the reference's Barrier ensures (spin_the_wheel.py:126-139)
+    lag_final = r[r[:, 2] == 1, 6]
+    assert np.isfinite(lag_final).all() and np.all(lag_final == lag_final[0])
+    assert ob >= lag_final[0], (ob, lag_final[0])
