@@ -80,7 +80,11 @@ typedef struct {
                               kernel (error if no compiled instance fits),
                               3 workgroup-per-scenario kernel (large scenarios),
                               4 shared-matrix streaming kernel (the only path, and
-                              the automatic one, of a PHGPU_SHARED_MATRIX handle) [0] */
+                              the automatic one, of a PHGPU_SHARED_MATRIX handle),
+                              5 pattern-specialised kernel: one lane per scenario,
+                              compiled with hipRTC for this handle's pattern at its
+                              first path-5 solve (n, m <= 48, nnz <= 128; that solve
+                              synchronises the stream once)               [0] */
     int32_t infeas_start;  /* infeasibility certificates are tested at the KKT
                               checks from this iteration on (< 0: never)      [512] */
     double eps_infeas;     /* certificate tolerance: ray violation <= eps * |ray
@@ -226,13 +230,15 @@ int phgpu_last_error(char* buf, size_t len);
 /* Workspace bytes held by the handle (diagnostics / memory planning). */
 int64_t phgpu_workspace_bytes(phgpu_handle h);
 
-/* Solve-kernel selection of the handle (diagnostics): info[18] =
+/* Solve-kernel selection of the handle (diagnostics): info[20] =
  * {register path (L <= 64 lanes per scenario): instance or -1, L, column slots / CSC
  *  entries per column / row slots / CSR entries per row needed, the instance's KC, ZC, KR,
  *  ZR;  workgroup path (one workgroup per scenario): instance or -1, waves per scenario,
  *  KC, ZC, KR, ZR;  the default path of phgpu_solve: 1 global, 2 register, 3 workgroup,
- *  4 shared-matrix streaming;  the queue mode of the last register-path solve: 1 record
- *  mode (longest-first queue, scenario-major records), 0 scenario order, -1 none yet}. */
+ *  4 shared-matrix streaming, 5 pattern-specialised;  the queue mode of the last
+ *  register-path solve: 1 record mode (longest-first queue, scenario-major records), 0
+ *  scenario order, -1 none yet;  1 if path 5 applies to the pattern;  the waves per SIMD
+ *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
 #ifdef __cplusplus

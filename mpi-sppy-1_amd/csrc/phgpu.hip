@@ -22,6 +22,7 @@
 #include <new>
 #include <stdlib.h>
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "phgpu.h"
@@ -50,6 +51,8 @@ static int set_err(int code, const char* fmt, ...) {
     } while (0)
 
 // ------------------------------------------------------------------ state
+struct jit_module;  // solve_jit.inc: the hipRTC-compiled path-5 kernel of a handle
+
 struct phgpu_state {
     int device;
     int64_t S;
@@ -135,6 +138,10 @@ struct phgpu_state {
     double *xw, *yw, *omega_w;
     int32_t* its_w;
     int pk_XW, pk_YW;
+    // path 5 (solve_jit.inc): the pattern-specialised module, and whether the column /
+    // row kinds it was built for still describe the data (reset by phgpu_set_scenarios)
+    jit_module* jit;
+    int jit_kinds_valid;
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -838,6 +845,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 #include "solve_reg.inc"
 #include "solve_wg.inc"
 #include "solve_stream.inc"
+#include "solve_jit.inc"
 
 // ------------------------------------------------------------------ PH reductions
 // phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
@@ -1980,6 +1988,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     h->pending = -1;
     h->have_s[0] = h->have_s[1] = 0;
     h->warm_rec_s[0] = h->warm_rec_s[1] = 0;
+    h->jit_kinds_valid = 0;
     bind_slots(h);
     HIPCHK(run_setup(h, st));
     // the setup's start omega (slot 0) for slot 1 too
@@ -2028,6 +2037,16 @@ extern "C" int phgpu_commit(phgpu_handle h) {
     return 0;
 }
 
+// the path phgpu_solve takes for kernel 0 (gamma = 1): the pattern-specialised kernel
+// (path 5) where it applies and PHGPU_JIT does not turn it off (PHGPU_JIT=0), else the
+// path chosen at phgpu_create
+static int default_path(const phgpu_state* h) {
+    const char* env = getenv("PHGPU_JIT");
+    if (env && atoi(env) == 0) return h->default_kernel;
+    if (jit_eligible(h) && (env || h->S >= JIT_MIN_S)) return 5;
+    return h->default_kernel;
+}
+
 static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
                       double* obj, double* bound, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return set_err(-1, "null handle");
@@ -2070,10 +2089,10 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     hipStream_t st = (hipStream_t)stream;
     // the register-resident kernels are specialised for the reflected step (gamma = 1, the
     // default); another gamma runs on the global-memory kernel
-    if (o.kernel < 0 || o.kernel > 4) return set_err(-1, "bad kernel option %d", o.kernel);
+    if (o.kernel < 0 || o.kernel > 5) return set_err(-1, "bad kernel option %d", o.kernel);
     if (h->shared != (o.kernel == 4 || (o.kernel == 0 && h->shared)))
         return set_err(-1, "kernel option %d: a shared-matrix handle solves with path 4 only (kernel 0 or 4), "
-                       "other handles with paths 1-3", o.kernel);
+                       "other handles with paths 1-3 and 5", o.kernel);
     if (h->shared) {
         if (!h->scen_set) return set_err(-1, "phgpu_set_scenarios has not been called");
         int per_cu = 0;
@@ -2111,9 +2130,12 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         return set_err(-1, "register-resident kernel requested but no compiled instance fits this pattern");
     if (o.kernel == 3 && h->wg_inst < 0)
         return set_err(-1, "workgroup-per-scenario kernel requested but no compiled instance fits this pattern");
-    if ((o.kernel == 2 || o.kernel == 3) && o.gamma != 1.0)
+    if ((o.kernel == 2 || o.kernel == 3 || o.kernel == 5) && o.gamma != 1.0)
         return set_err(-1, "register-resident kernels require gamma = 1 (got %g)", o.gamma);
-    const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? h->default_kernel : 1);
+    if (o.kernel == 5 && !jit_eligible(h))
+        return set_err(-1, "kernel 5 (pattern-specialised) needs n <= %d, m <= %d, nnz <= %d (got %d, %d, %d)",
+                       JIT_MAX_N, JIT_MAX_M, JIT_MAX_NNZ, h->n, h->m, h->nnz);
+    const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? default_path(h) : 1);
     const bool use_reg = path == 2;
     int out_rec = 0;  // the warm state this solve writes lives in the records
     if (path == 3 && !h->pk) {
@@ -2246,7 +2268,14 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             HIPCHK(from_records(h, h->pk_X, -1, h->n, h->x, st));
             HIPCHK(from_records(h, h->pk_Y, -1, h->m, h->y, st));
         }
-        hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+        if (path == 5) {
+            const int rc5 = jit_prepare(h, st);
+            if (rc5) return rc5;
+            const int rc6 = jit_launch(h, P, x, y, obj, bound, status, iters, st);
+            if (rc6) return rc6;
+        } else {
+            hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
+        }
         out_rec = 0;
     }
     HIPCHK(hipGetLastError());
@@ -2385,6 +2414,10 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->sk_bins, h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->jit) {
+        if (h->jit->mod) (void)hipModuleUnload(h->jit->mod);
+        delete h->jit;
+    }
     if (!h->shared) {  // warm-start slot 1 (slot 0 is x / y / omega / sk_iters above)
         void* slot1[] = {h->xs[1], h->ys[1], h->oms[1], h->its_s[1]};
         for (void* p : slot1)
@@ -2408,7 +2441,9 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     // info[0..9]: the register path (L <= 64); info[10..15]: the workgroup path; info[16]:
     // the path phgpu_solve takes by default (1 global, 2 register, 3 workgroup); info[17]:
     // queue mode of the last register-path solve (1 record mode, 0 scenario order, -1 none)
-    for (int k = 0; k < 18; ++k) info[k] = 0;
+    for (int k = 0; k < 20; ++k) info[k] = 0;
+    info[18] = jit_eligible(h) ? 1 : 0;
+    info[19] = h->jit ? h->jit->wpe : 0;
     info[17] = h->last_rec;
     info[0] = h->reg_inst;
     info[1] = h->reg_inst >= 0 ? h->reg_L : 0;
@@ -2432,6 +2467,6 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
         info[14] = g.KR;
         info[15] = g.ZR;
     }
-    info[16] = h->default_kernel;
+    info[16] = h->scen_set && !h->shared ? default_path(h) : h->default_kernel;
     return 0;
 }

@@ -157,10 +157,10 @@ class PHEngine:
 
     def kernel_info(self):
         """Which solve kernel the handle uses (phgpu_kernel_info)."""
-        info = (ctypes.c_int32 * 18)()
+        info = (ctypes.c_int32 * 20)()
         _lib.check(self.lib.phgpu_kernel_info(self.h, info), "phgpu_kernel_info")
         keys = ["instance", "lanes", "kc", "zc", "kr", "zr", "KC", "ZC", "KR", "ZR",
-                "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path", "rec"]
+                "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path", "rec", "jit_eligible", "jit_wpe"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state
@@ -195,7 +195,7 @@ class PHEngine:
         by bench.py for the per-launch roofline inside its timed region."""
         self._ins = {"events": [], "iters": torch.empty((max_solves, self.S), dtype=torch.int32,
                                                          device=self.device),
-                     "not_optimal": torch.zeros(max_solves, dtype=torch.int64, device=self.device),
+                     "counts": torch.zeros((max_solves, 4), dtype=torch.int32, device=self.device),
                      "ar_events": []}
 
     def instrumented(self):
@@ -213,7 +213,7 @@ class PHEngine:
         ins = getattr(self, "_ins", None)
         if not ins:
             return []
-        return ins["not_optimal"][:len(ins["events"])].cpu().tolist()
+        return ins["counts"][:len(ins["events"]), 1:].sum(dim=1).cpu().tolist()
 
     def instrumented_allreduce_ms(self):
         """Total ms of the x̄ / conv all-reduces issued while instrumenting (HIP events on
@@ -267,7 +267,10 @@ class PHEngine:
             ev[1].record()
             k = len(ins["events"])
             ins["iters"][k].copy_(out["iters"])
-            ins["not_optimal"][k] = (out["status"] != 0).sum()
+            # status counts of this launch by the library's one-block reduction (a torch
+            # reduction here stalls the host ~2 ms per call)
+            _lib.check(self.lib.phgpu_status_counts(self.h, _ptr(out["status"]), _ptr(ins["counts"][k]),
+                                                    self._stream()), "phgpu_status_counts")
             ins["events"].append(ev)
             ins.setdefault("spec", []).append(speculative)
 
