@@ -224,7 +224,44 @@ def _latest_profile_file(name, pdir=None):
     return None
 
 
-def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
+def ipm_flops_per_iter(b, ipm):
+    """Algorithmic fp64 flops of one path-6 iteration of one scenario (one Newton solve,
+    DESIGN.md 3.7): A x and A'y (4 nnz), the KKT test (12 n + 6 m), slacks, reciprocals
+    and mu (7 per finite bound side), D and E (5 per column / row), the normal-equation
+    assembly (k(k+1) + k per column of k entries), the LDL' factorisation and one forward
+    + backward solve (counted by the library from the symbolic factor), the right-hand
+    side (2 nnz + 14 n + 8 m), dx and dw (4 nnz + 3 n + m), step lengths (8 per side) and
+    the update (6 per side + 2 n + 4 m)."""
+    n, m, nnz = b.n, b.m, b.nnz
+    k = np.bincount(np.asarray(b.col_idx), minlength=n)
+    eq = (b.rl[0] == b.ru[0])
+    sides = int(np.isfinite(b.lb[0]).sum() + np.isfinite(b.ub[0]).sum()
+                + (np.isfinite(b.rl[0]) & ~eq).sum() + (np.isfinite(b.ru[0]) & ~eq).sum())
+    return (4 * nnz + 12 * n + 6 * m + 7 * sides + 5 * (n + m) + int((k * (k + 1) + k).sum())
+            + ipm["factor_flops"] + ipm["solve_flops"] + 2 * nnz + 14 * n + 8 * m + 4 * nnz + 3 * n + m
+            + 8 * sides + 6 * sides + 2 * n + 4 * m)
+
+
+def roofline_ipm(b, ipm, launches, ws_bytes):
+    """Roofline of the interior-point kernel (path 6): fp64 issue-bound like the other
+    register-resident paths (each lane holds its scenario's whole IPM state), achieved =
+    ipm_flops_per_iter x IPM iterations per launch / mean HIP-event launch time."""
+    launch_ms = float(np.mean([t for t, _ in launches]))
+    units = float(np.mean([u for _, u in launches]))
+    F = ipm_flops_per_iter(b, ipm)
+    tflops = F * units / (launch_ms * 1e-3) / 1e12
+    return {"bound": "fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "traffic_source": None,
+            "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
+            "kernel": "k_solve_ipm (hipRTC, pattern-specialised)", "lanes_per_scenario": 1,
+            "launch_ms": launch_ms, "scenario_iters_per_launch": units, "flops_per_scenario_iter": F,
+            "ipm": {k: ipm[k] for k in ("rows", "factor_entries", "scratch_bytes", "compile_s")},
+            "note": ("achieved = F x IPM scenario-iterations per launch / mean HIP-event launch time (the "
+                     "launch includes the PDHG fallback kernel over the IPM's fallback list); F = "
+                     "ipm_flops_per_iter (bench.py)")}
+
+
+def roofline(b, kinfo, launches, ws_bytes, tag, pdir, ipm=None):
     """Roofline of the solve kernel.
 
     The register-resident kernels keep each scenario's iterate in VGPRs / LDS for the
@@ -245,6 +282,8 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir):
         lanes = 64 * kinfo["wps"]
     elif path == 4:
         return roofline_stream(b, launches, ws_bytes, tag, pdir)
+    elif path == 6:
+        return roofline_ipm(b, ipm, launches, ws_bytes)
     else:
         kname, lanes = "k_solve", 1
     launch_ms = float(np.mean([t for t, _ in launches]))
@@ -487,7 +526,7 @@ def main():
     comm.allreduce_sum_(n_bad)
     kinfo = e.kernel_info()
     ws = e.workspace_bytes() + 8 * (b.S * (b.n + b.m + 3 * max(b.nn, 1) + 4))
-    rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir)
+    rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir, ipm=e.ipm_info())
     ph_its = a.steps / elapsed
     if rank == 0:
         out = {
@@ -518,7 +557,8 @@ def main():
                                        (f" ({'RCCL' if backend == 'nccl' else 'gloo, ranks sharing a GPU'}"
                                         f" x̄ all-reduce)" if world > 1 else ""))},
             "solves_per_sec": ph_its * a.scens,
-            "pdhg_iters_per_ph_iter": {"max": int(it_host.max()), "mean": float(it_host.mean())},
+            "solver": "ipm" if kinfo["path"] == 6 else "pdhg",
+            "solver_iters_per_ph_iter": {"max": int(it_host.max()), "mean": float(it_host.mean())},
             "time_split_ms": {"solve_launch": rl["launch_ms"],
                               "allreduce": float(ar_ms.item()),
                               "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"] - float(ar_ms.item())},

@@ -84,7 +84,14 @@ typedef struct {
                               5 pattern-specialised kernel: one lane per scenario,
                               compiled with hipRTC for this handle's pattern at its
                               first path-5 solve (n, m <= 48, nnz <= 128; that solve
-                              synchronises the stream once)               [0] */
+                              synchronises the stream once),
+                              6 interior-point kernel (Mehrotra predictor-corrector,
+                              one lane per scenario, compiled with hipRTC for this
+                              handle's pattern and data at its first path-6 solve, which
+                              synchronises once; n <= 40, m <= 32, nnz <= 128; the
+                              automatic path wherever it applies, PHGPU_IPM=0 turns that
+                              off; scenarios it does not finish go to the path-5 PDHG,
+                              which certifies infeasibility)              [0] */
     int32_t infeas_start;  /* infeasibility certificates are tested at the KKT
                               checks from this iteration on (< 0: never)      [512] */
     double eps_infeas;     /* certificate tolerance: ray violation <= eps * |ray
@@ -159,7 +166,8 @@ int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
  *   bound[S]     device out: Lagrangian dual bound (results.Problem[0].Lower_bound,
  *                spopt.py:201-206)
  *   status[S]    device out: PHGPU_* code
- *   iters[S]     device out (may be NULL): PDHG iterations used                 */
+ *   iters[S]     device out (may be NULL): iterations used (PDHG iterations; interior-
+ *                point iterations for scenarios path 6 solved)                  */
 int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
                 double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
                 void* stream);
@@ -235,11 +243,30 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  *  entries per column / row slots / CSR entries per row needed, the instance's KC, ZC, KR,
  *  ZR;  workgroup path (one workgroup per scenario): instance or -1, waves per scenario,
  *  KC, ZC, KR, ZR;  the default path of phgpu_solve: 1 global, 2 register, 3 workgroup,
- *  4 shared-matrix streaming, 5 pattern-specialised;  the queue mode of the last
+ *  4 shared-matrix streaming, 5 pattern-specialised, 6 interior point;  the queue mode of the last
  *  register-path solve: 1 record mode (longest-first queue, scenario-major records), 0
  *  scenario order, -1 none yet;  1 if path 5 applies to the pattern;  the waves per SIMD
  *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
+
+/* Path-6 (interior point) diagnostics: info[10] = {1 if path 6 applies to the pattern,
+ * factor entries of the pattern with every row active, 1 if a compiled module spilled
+ * (path 6 is then not the automatic path), 1 if a module is compiled, rows in its normal
+ * equations, its factor entries, its scratch bytes per lane, its hipRTC compile seconds,
+ * flops of one LDL' factorisation, flops of one forward + backward solve}. */
+int phgpu_ipm_info(phgpu_handle h, double* info);
+
+/* The path-6 source the library generates for a pattern and its data flags (host code
+ * only; tests and tools).  flags / v0 are per element of [A nnz | c n | q n | lb n | ub n |
+ * rl m | ru m]: bit 0 the same value in every scenario, bit 1 finite in some scenario,
+ * bit 2 finite in every scenario, bit 3 (rl elements) rl == ru in every scenario; v0 the
+ * first scenario's value.  nonant_slot[n]: nonant index of each column or -1.  Writes the
+ * NUL-terminated source to buf when len exceeds its length; returns the length + 1 (or a
+ * negative error); info[4] (may be NULL) = {rows in the normal equations, factor entries,
+ * factorisation flops, solve flops}. */
+int phgpu_ipm_source(int32_t n, int32_t m, int32_t nnz, const int32_t* row_ptr, const int32_t* col_idx,
+                     const int32_t* nonant_slot, const int32_t* flags, const double* v0, char* buf, size_t len,
+                     int32_t* info);
 
 #ifdef __cplusplus
 }

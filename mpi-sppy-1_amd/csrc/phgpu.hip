@@ -52,6 +52,7 @@ static int set_err(int code, const char* fmt, ...) {
 
 // ------------------------------------------------------------------ state
 struct jit_module;  // solve_jit.inc: the hipRTC-compiled path-5 kernel of a handle
+struct ipm_module;  // solve_ipm.inc: the hipRTC-compiled path-6 module of a handle
 
 struct phgpu_state {
     int device;
@@ -142,6 +143,13 @@ struct phgpu_state {
     // row kinds it was built for still describe the data (reset by phgpu_set_scenarios)
     jit_module* jit;
     int jit_kinds_valid;
+    // path 6 (solve_ipm.inc): the interior-point module; whether the data flags it was
+    // built for still hold (reset by phgpu_set_scenarios); factor entries of the pattern
+    // (0: not eligible); 1 once a compiled module spilled (path 6 is then not the
+    // default); the fallback list [S] and its counters {fail_n[2], qhead[2]} by parity
+    ipm_module* ipm;
+    int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity;
+    int32_t *ipm_list, *ipm_cnt;
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -846,6 +854,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 #include "solve_wg.inc"
 #include "solve_stream.inc"
 #include "solve_jit.inc"
+#include "solve_ipm.inc"
 
 // ------------------------------------------------------------------ PH reductions
 // phbase.py:54-79: per-wave partial sums of prob_coeff * x and prob_coeff * x^2 for
@@ -1644,6 +1653,17 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         ALLOC(h->yt, (size_t)m * Sz);
     }
     ALLOC(h->qhead, 1);
+    if (!h->shared) {  // path 6: the pattern's factor size, the fallback list and its counters
+        h->ipm_nf = ipm_nf_bound(n, m, row_ptr, col_idx);
+        if (h->ipm_nf > 0) {
+            ALLOC(h->ipm_list, Sz);
+            ALLOC(h->ipm_cnt, 4);
+            if (hipMemset(h->ipm_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess) {
+                phgpu_destroy(h);
+                return set_err(-2, "hipMemset failed");
+            }
+        }
+    }
     // warm-start slots: slot 0 is the arrays above; slot 1 (deferred solves, paths 1-3)
     h->xs[0] = h->x;
     h->ys[0] = h->y;
@@ -1989,6 +2009,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     h->have_s[0] = h->have_s[1] = 0;
     h->warm_rec_s[0] = h->warm_rec_s[1] = 0;
     h->jit_kinds_valid = 0;
+    h->ipm_flags_valid = 0;
     bind_slots(h);
     HIPCHK(run_setup(h, st));
     // the setup's start omega (slot 0) for slot 1 too
@@ -2037,10 +2058,13 @@ extern "C" int phgpu_commit(phgpu_handle h) {
     return 0;
 }
 
-// the path phgpu_solve takes for kernel 0 (gamma = 1): the pattern-specialised kernel
-// (path 5) where it applies and PHGPU_JIT does not turn it off (PHGPU_JIT=0), else the
-// path chosen at phgpu_create
+// the path phgpu_solve takes for kernel 0 (gamma = 1): the interior-point kernel (path 6)
+// where it applies (PHGPU_IPM=0 turns it off, a module that spills takes it out), then
+// the pattern-specialised PDHG kernel (path 5) when PHGPU_JIT asks for it, else the path
+// chosen at phgpu_create
 static int default_path(const phgpu_state* h) {
+    const char* ie = getenv("PHGPU_IPM");
+    if (ipm_eligible(h) && !h->ipm_off && !(ie && atoi(ie) == 0)) return 6;
     const char* env = getenv("PHGPU_JIT");
     if (env && atoi(env) == 0) return h->default_kernel;
     if (jit_eligible(h) && (env || h->S >= JIT_MIN_S)) return 5;
@@ -2089,10 +2113,10 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     hipStream_t st = (hipStream_t)stream;
     // the register-resident kernels are specialised for the reflected step (gamma = 1, the
     // default); another gamma runs on the global-memory kernel
-    if (o.kernel < 0 || o.kernel > 5) return set_err(-1, "bad kernel option %d", o.kernel);
+    if (o.kernel < 0 || o.kernel > 6) return set_err(-1, "bad kernel option %d", o.kernel);
     if (h->shared != (o.kernel == 4 || (o.kernel == 0 && h->shared)))
         return set_err(-1, "kernel option %d: a shared-matrix handle solves with path 4 only (kernel 0 or 4), "
-                       "other handles with paths 1-3 and 5", o.kernel);
+                       "other handles with paths 1-3, 5 and 6", o.kernel);
     if (h->shared) {
         if (!h->scen_set) return set_err(-1, "phgpu_set_scenarios has not been called");
         int per_cu = 0;
@@ -2135,7 +2159,19 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     if (o.kernel == 5 && !jit_eligible(h))
         return set_err(-1, "kernel 5 (pattern-specialised) needs n <= %d, m <= %d, nnz <= %d (got %d, %d, %d)",
                        JIT_MAX_N, JIT_MAX_M, JIT_MAX_NNZ, h->n, h->m, h->nnz);
-    const int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? default_path(h) : 1);
+    if (o.kernel == 6 && !ipm_eligible(h))
+        return set_err(-1, "kernel 6 (interior point) needs n <= %d, m <= %d, nnz <= %d and <= %d factor entries "
+                       "(got %d, %d, %d, %d)", IPM_MAX_N, IPM_MAX_M, IPM_MAX_NNZ, IPM_MAX_NF, h->n, h->m, h->nnz,
+                       h->ipm_nf);
+    int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? default_path(h) : 1);
+    if (path == 6) {
+        const int rc6 = ipm_prepare(h, st);
+        if (rc6) return rc6;
+        if (o.kernel == 0 && h->ipm->private_bytes > IPM_SPILL_MAX) {
+            h->ipm_off = 1;  // the automatic choice falls back to the handle's PDHG path
+            path = default_path(h);
+        }
+    }
     const bool use_reg = path == 2;
     int out_rec = 0;  // the warm state this solve writes lives in the records
     if (path == 3 && !h->pk) {
@@ -2272,6 +2308,9 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             const int rc5 = jit_prepare(h, st);
             if (rc5) return rc5;
             const int rc6 = jit_launch(h, P, x, y, obj, bound, status, iters, st);
+            if (rc6) return rc6;
+        } else if (path == 6) {
+            const int rc6 = ipm_launch(h, P, x, y, obj, bound, status, iters, st);
             if (rc6) return rc6;
         } else {
             hipLaunchKernelGGL(k_solve, grid_for(h->S), dim3(BLOCK), 0, st, *h, P, x, y, obj, bound, status, iters);
@@ -2418,6 +2457,12 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
         if (h->jit->mod) (void)hipModuleUnload(h->jit->mod);
         delete h->jit;
     }
+    if (h->ipm) {
+        if (h->ipm->mod) (void)hipModuleUnload(h->ipm->mod);
+        delete h->ipm;
+    }
+    if (h->ipm_list) (void)hipFree(h->ipm_list);
+    if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
     if (!h->shared) {  // warm-start slot 1 (slot 0 is x / y / omega / sk_iters above)
         void* slot1[] = {h->xs[1], h->ys[1], h->oms[1], h->its_s[1]};
         for (void* p : slot1)
@@ -2468,5 +2513,23 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
         info[15] = g.ZR;
     }
     info[16] = h->scen_set && !h->shared ? default_path(h) : h->default_kernel;
+    return 0;
+}
+
+extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
+    if (!h || !info) return set_err(-1, "null argument");
+    for (int k = 0; k < 10; ++k) info[k] = 0.0;
+    info[0] = ipm_eligible(h) ? 1.0 : 0.0;
+    info[1] = h->ipm_nf;
+    info[2] = h->ipm_off;
+    if (h->ipm) {
+        info[3] = 1.0;
+        info[4] = h->ipm->mr;
+        info[5] = h->ipm->nf;
+        info[6] = h->ipm->private_bytes;
+        info[7] = h->ipm->compile_s;
+        info[8] = h->ipm->fac_flops;
+        info[9] = h->ipm->sol_flops;
+    }
     return 0;
 }

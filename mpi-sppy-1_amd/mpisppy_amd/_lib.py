@@ -47,7 +47,7 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_solve", "phgpu_solve_deferred", "phgpu_commit", "phgpu_ph_reduce", "phgpu_ph_update",
            "phgpu_expectations",
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
-           "phgpu_kernel_info"]
+           "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source"]
 
 _lib = None
 
@@ -86,6 +86,9 @@ def load(path=None):
     lib.phgpu_workspace_bytes.argtypes = [c_vp]
     lib.phgpu_workspace_bytes.restype = c_i64
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
+    lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
+    lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl),
+                                     ctypes.c_char_p, ctypes.c_size_t, P_i32]
     for name in EXPORTS:
         if name != "phgpu_workspace_bytes":
             getattr(lib, name).restype = c_int
@@ -104,6 +107,52 @@ def last_error():
 def check(rc, what):
     if rc != 0:
         raise PhgpuError(f"{what} failed (rc={rc}): {last_error()}")
+
+
+# element flags of phgpu_ipm_source (include/phgpu.h)
+IPMF_UNI, IPMF_FIN_ANY, IPMF_FIN_ALL, IPMF_EQ = 1, 2, 4, 8
+
+
+def ipm_flags(batch):
+    """Host restatement of the library's k_ipm_flags over a ScenarioBatch (for
+    phgpu_ipm_source in tests / tools): flags and first-scenario values per element of
+    [A nnz | c n | q n | lb n | ub n | rl m | ru m]."""
+    import numpy as np
+    parts = [batch.A_val, batch.c, batch.q, batch.lb, batch.ub, batch.rl, batch.ru]
+    flags, v0 = [], []
+    for pi, arr in enumerate(parts):
+        a = np.asarray(arr, dtype=np.float64)
+        bits = a.view(np.int64)
+        uni = (bits == bits[:1]).all(0)
+        fin = np.isfinite(a)
+        f = uni * IPMF_UNI + fin.any(0) * IPMF_FIN_ANY + fin.all(0) * IPMF_FIN_ALL
+        if pi == 5:
+            f = f + (fin & (np.asarray(batch.ru) == a)).all(0) * IPMF_EQ
+        flags.append(f.astype(np.int32))
+        v0.append(a[0])
+    return np.concatenate(flags).astype(np.int32), np.concatenate(v0).astype(np.float64)
+
+
+def ipm_source(batch):
+    """The path-6 source the library generates for a batch (no GPU): (text, (rows, factor
+    entries, factorisation flops, solve flops))."""
+    import numpy as np
+    lib = load()
+    flags, v0 = ipm_flags(batch)
+    slot = np.full(batch.n, -1, dtype=np.int32)
+    slot[batch.nonant_col] = np.arange(batch.nn, dtype=np.int32)
+    rp = np.ascontiguousarray(batch.row_ptr, dtype=np.int32)
+    ci = np.ascontiguousarray(batch.col_idx, dtype=np.int32)
+    ip = lambda a: a.ctypes.data_as(P_i32)  # noqa: E731
+    info = np.zeros(4, dtype=np.int32)
+    args = (batch.n, batch.m, batch.nnz, ip(rp), ip(ci), ip(slot), ip(flags),
+            v0.ctypes.data_as(ctypes.POINTER(c_dbl)))
+    need = lib.phgpu_ipm_source(*args, None, 0, ip(info))
+    if need < 0:
+        raise PhgpuError(f"phgpu_ipm_source failed: {last_error()}")
+    buf = ctypes.create_string_buffer(need + 1)
+    lib.phgpu_ipm_source(*args, buf, need + 1, ip(info))
+    return buf.value.decode(), tuple(int(v) for v in info)
 
 
 def default_options(**overrides):

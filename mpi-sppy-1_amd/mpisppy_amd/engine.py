@@ -163,6 +163,14 @@ class PHEngine:
                 "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path", "rec", "jit_eligible", "jit_wpe"]
         return dict(zip(keys, list(info)))
 
+    def ipm_info(self):
+        """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
+        info = (ctypes.c_double * 10)()
+        _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
+        keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
+                "factor_flops", "solve_flops"]
+        return dict(zip(keys, list(info)))
+
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):
         """rho: scalar, host [nn] array (the same per-nonant rho in every scenario) or host

@@ -22,6 +22,19 @@ def _gpu_selected(config):
     return "gpu" in expr and "not" not in expr
 
 
+@pytest.fixture
+def register_path():
+    """Keep the handles of the test on their PDHG path: PHGPU_IPM=0 takes the
+    interior-point path 6 out of the automatic choice (the library reads it per solve)."""
+    keep = os.environ.get("PHGPU_IPM")
+    os.environ["PHGPU_IPM"] = "0"
+    yield
+    if keep is None:
+        os.environ.pop("PHGPU_IPM", None)
+    else:
+        os.environ["PHGPU_IPM"] = keep
+
+
 @pytest.fixture(scope="session")
 def gpu(request):
     """The MI355X. Under ``-m gpu`` a missing device FAILS the test: a GPU box whose torch

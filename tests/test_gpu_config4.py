@@ -56,9 +56,10 @@ def _assert_bench_instance(ph):
 
 @pytest.fixture
 def pinned_l8_record_mode():
-    keep = {k: os.environ.get(k) for k in ("PHGPU_LANES", "PHGPU_REG_REC")}
+    keep = {k: os.environ.get(k) for k in ("PHGPU_LANES", "PHGPU_REG_REC", "PHGPU_IPM")}
     os.environ["PHGPU_LANES"] = "8"
     os.environ["PHGPU_REG_REC"] = "1"
+    os.environ["PHGPU_IPM"] = "0"
     yield
     for k, v in keep.items():
         if v is None:
@@ -86,7 +87,7 @@ def test_aircond432_on_the_bench_instance(gpu, pinned_l8_record_mode):
 
 
 @pytest.mark.skipif(not os.path.exists(SCALE_FILE), reason="aircond_scale.json not generated")
-def test_config4_aircond65536_vs_oracle(gpu):
+def test_config4_aircond65536_vs_oracle(gpu, register_path):
     g = json.load(open(SCALE_FILE))
     assert g["kwargs"] == KW and g["rho"] == 1.0
     ph = _aircond_ph(g["branching_factors"], g["ph_iters"], -1.0)

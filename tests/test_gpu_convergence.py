@@ -46,12 +46,27 @@ def _record_conv(ph):
     return seen
 
 
-@pytest.mark.parametrize("eps_rel,w_tol", [(1e-9, 1e-4), (1e-10, ABS)])
-def test_config3_iterations_to_convergence(gpu, eps_rel, w_tol):
+@pytest.mark.parametrize("path,eps_rel,w_tol", [(6, 1e-9, ABS), (2, 1e-9, 1e-4), (2, 1e-10, ABS)])
+def test_config3_iterations_to_convergence(gpu, path, eps_rel, w_tol):
     """eps_rel 1e-9 is the bench's PH-subproblem tolerance: iterations, conv and x̄ meet
     the north_star bars, W (the sum of 1,078 solves' rho (x - x̄)) stays within 1e-4 of
     the exact oracle (4.7e-5 measured on one of 1,024 sampled scenarios, ~3e-7 typical);
-    with the subproblems at 1e-10 W meets 1e-5 too."""
+    with the subproblems at 1e-10 W meets 1e-5 too.  Path 6 (the interior point, the
+    default for this pattern since round 3) presses each solve to 1e-13 and meets 1e-5 at
+    the bench's 1e-9; path 2 (the register PDHG) runs with PHGPU_IPM=0."""
+    keep = os.environ.get("PHGPU_IPM")
+    if path == 2:
+        os.environ["PHGPU_IPM"] = "0"
+    try:
+        _run_convergence(path, eps_rel, w_tol)
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_IPM", None)
+        else:
+            os.environ["PHGPU_IPM"] = keep
+
+
+def _run_convergence(path, eps_rel, w_tol):
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     S = CONV["S"]
@@ -65,7 +80,12 @@ def test_config3_iterations_to_convergence(gpu, eps_rel, w_tol):
     tb = ph.Iter0()
     assert abs(tb - CONV["trivial_bound"]) <= 1e-5 * abs(CONV["trivial_bound"])
     info = ph.engine.kernel_info()
-    assert info["lanes"] == 4 and (info["KC"], info["ZC"], info["KR"], info["ZR"]) == (3, 3, 2, 4), info
+    assert info["path"] == path, info
+    if path == 2:
+        assert info["lanes"] == 4 and (info["KC"], info["ZC"], info["KR"], info["ZR"]) == (3, 3, 2, 4), info
+    else:
+        ii = ph.engine.ipm_info()
+        assert ii["compiled"] == 1 and ii["scratch_bytes"] == 0, ii
     seen = _record_conv(ph)
     ph.iterk_loop()
     assert ph._speculate(False), "the bench's loop variant (speculative solve) must be the one tested"

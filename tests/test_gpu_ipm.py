@@ -1,0 +1,175 @@
+"""Path 6: the batched interior-point solve (csrc/solve_ipm.inc, jit_ipm.hip.in), compiled
+at run time with hipRTC for the handle's pattern and data, and the automatic path for
+farmer cm = 1 (the headline, config 3).  Checked against the same oracle and fixtures as
+the PDHG paths:
+
+  * the reference's farmer fixtures (w_test_data: W and x̄ after 5 PH iterations);
+  * config 3's headline fixture on the full 65,536 scenarios with the bench's options
+    (trivial bound, 1,024 Iter0 objectives, x̄ and conv of 5 iterations, sampled W,
+    E[obj]) -- the instance bench.py times;
+  * aircond bf 4-3-2 (multistage, equality rows, a diagonal quadratic in the model);
+  * random LP / QP batches with ranged, equality, one-sided and free rows and infinite
+    bounds against HiGHS / the oracle's IPM (per-scenario data of every kind);
+  * infeasible / unbounded scenarios: the IPM hands them to the path-5 PDHG fallback,
+    which certifies them; the IPM iteration cap routes every scenario through the
+    fallback and the answers stay the oracle's;
+  * nonant fixing (Xhat evaluation) against the register path.
+Tolerances (north_star): objectives 1e-5 relative, x̄ / W 1e-5 absolute, iterations +-1.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import _ph, _random_lp_batch, GOLD, OBJ_REL, ABS
+from test_gpu_scale import SCALE, _farmer_ph, _run_and_compare, _tiny_batch
+
+pytestmark = pytest.mark.gpu
+K6 = {"kernel": 6}
+
+
+def _assert_path6(engine, scratch_free=True):
+    info, ii = engine.kernel_info(), engine.ipm_info()
+    assert ii["compiled"] == 1, ii
+    if scratch_free:
+        assert info["path"] == 6 and ii["scratch_bytes"] == 0 and ii["off"] == 0, (info, ii)
+
+
+def test_farmer3_reference_fixtures_on_path6(gpu):
+    from mpisppy_amd.examples import farmer
+    names = farmer.scenario_names_creator(3)
+    ph = _ph(names, farmer.scenario_creator, {"num_scens": 3})
+    conv, eobj, tb = ph.ph_main()
+    _assert_path6(ph.engine)
+    g = GOLD["farmer3_rho1"]
+    assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
+    assert np.abs(ph.W_array() - np.array(g["traj"][4]["W"])).max() <= ABS
+    assert np.abs(ph.xbar_by_node()["ROOT"][:3] - np.array(g["traj"][4]["xbar"])).max() <= ABS
+
+
+def test_headline_farmer65536_on_path6(gpu):
+    """Config 3 exactly as bench.py runs it (automatic path = 6, the example's options)."""
+    from mpisppy_amd.examples import farmer
+    g = SCALE["farmer65536_cm1"]
+    names = [f"scen{i}" for i in range(65536)]
+    ph = _farmer_ph(names, 1, 65536, iterk_solver_options=dict(farmer.PDHG_ITERK_OPTIONS))
+    _run_and_compare(ph, g)
+    _assert_path6(ph.engine)
+    it = ph.engine.host("iters")
+    assert it.max() <= 60, it.max()  # interior-point iterations, not PDHG ones
+
+
+def test_aircond432_on_path6(gpu):
+    from mpisppy_amd.examples import aircond
+    from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+    g = GOLD["aircond432_rho1"]
+    kw = dict(g["kwargs"])
+    kw["branching_factors"] = g["branching_factors"]
+    nodes = create_nodenames_from_branching_factors(g["branching_factors"])
+    ph = _ph(g["names"], aircond.scenario_creator, kw, iters=5, all_nodenames=nodes,
+             batch_creator=aircond.batch_creator, iter0_solver_options=dict(K6), iterk_solver_options=dict(K6))
+    conv, eobj, tb = ph.ph_main()
+    _assert_path6(ph.engine, scratch_free=False)
+    assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
+    assert np.abs(ph.W_array() - np.array(g["traj5"][4]["W"])).max() <= ABS
+    ph2 = _ph(g["names"], aircond.scenario_creator, kw, iters=300, thresh=1e-4, all_nodenames=nodes,
+              batch_creator=aircond.batch_creator, iter0_solver_options=dict(K6), iterk_solver_options=dict(K6))
+    ph2.ph_main()
+    assert ph2.converged and abs(ph2._PHIter - g["conv_1e-4_iter"]) <= 1, (ph2._PHIter, g["conv_1e-4_iter"])
+
+
+@pytest.mark.parametrize("S,with_q", [(1, False), (67, False), (130, True), (300, True)])
+def test_random_batches_on_path6(gpu, S, with_q):
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    from oracle.lpqp import solve_lp_highs, solve_qp_ipm
+    b = _random_lp_batch(S, 9, 6, 0.5, seed=S + 7, with_q=with_q)
+    e = PHEngine(b, device="cuda:0")
+    e.solve(_lib.default_options(kernel=6), warm=False)
+    st, obj, bnd, x = e.host("status"), e.host("obj"), e.host("bound"), e.host("x")
+    assert (st == _lib.OPTIMAL).all(), st
+    for s in range(S):
+        A = b.dense_A(s)
+        if with_q:
+            xr, ob, rc = solve_qp_ipm(A, b.rl[s], b.ru[s], b.lb[s], b.ub[s], b.c[s], b.q[s])
+        else:
+            xr, ob, rc = solve_lp_highs(A, b.rl[s], b.ru[s], b.lb[s], b.ub[s], b.c[s])
+        assert rc == 0
+        tol = OBJ_REL * max(1.0, abs(ob))
+        assert abs(obj[s] - ob) <= tol and abs(bnd[s] - ob) <= tol, (s, obj[s], bnd[s], ob)
+        ax = A @ x[s]
+        assert np.all(ax >= b.rl[s] - 1e-6 * (1 + np.abs(b.rl[s])))
+        assert np.all(ax <= b.ru[s] + 1e-6 * (1 + np.abs(b.ru[s])))
+        assert np.all(x[s] >= b.lb[s] - 1e-9) and np.all(x[s] <= b.ub[s] + 1e-9)
+    # the same problems on the runtime-pattern PDHG kernel agree
+    e.solve(_lib.default_options(kernel=1), warm=False)
+    o1 = e.host("obj")
+    assert np.all(np.abs(o1 - obj) <= OBJ_REL * np.maximum(1.0, np.abs(o1)))
+    e.close()
+
+
+@pytest.mark.parametrize("kind,code", [("primal", 2), ("dual", 3)])
+def test_path6_hands_infeasible_scenarios_to_the_pdhg(gpu, kind, code):
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    S, bad = 70, 37
+    e = PHEngine(_tiny_batch(S, bad, kind), device="cuda:0")
+    e.solve(_lib.default_options(kernel=6), warm=False)
+    st, it, obj = e.host("status"), e.host("iters"), e.host("obj")
+    assert st[bad] == code, (st[bad], it[bad])
+    others = np.delete(np.arange(S), bad)
+    assert (st[others] == _lib.OPTIMAL).all()
+    assert np.isinf(obj[bad]) and (obj[bad] > 0) == (code == 2)
+    assert np.abs(obj[others] + 8.0).max() <= 1e-6
+    assert it[others].max() <= 60  # the IPM solved the others
+    e.close()
+
+
+def test_path6_fallback_for_every_scenario(gpu):
+    """PHGPU_IPM_MAXIT=2: every scenario leaves the IPM unfinished and the path-5 PDHG
+    solves the whole list (warm-started from the IPM's iterate); the answers are the
+    oracle's (config 3's fixture on a 4,096-scenario slice)."""
+    g = SCALE["farmer65536_cm1"]
+    os.environ["PHGPU_IPM_MAXIT"] = "2"
+    try:
+        names = [f"scen{i}" for i in range(0, 65536, 16)]
+        ph = _farmer_ph(names, 1, 65536)
+        ph.PH_Prep()
+        ph.Iter0()
+        st, it, obj = ph.engine.host("status"), ph.engine.host("iters"), ph.engine.host("obj")
+    finally:
+        del os.environ["PHGPU_IPM_MAXIT"]
+    assert (st == 0).all()
+    assert it.min() > 2  # PDHG iteration counts: every scenario went through the fallback
+    idx = [k for k, s in enumerate(range(0, 65536, 16)) if s in set(g["sample"])]
+    want = np.array([g["iter0_obj"][g["sample"].index(s)] for s in range(0, 65536, 16) if s in set(g["sample"])])
+    assert np.abs(obj[idx] - want).max() <= OBJ_REL * np.abs(want).max()
+
+
+def test_path6_fixed_nonants_match_register_path(gpu):
+    """Xhat-style evaluation: nonants fixed per scenario (phgpu_fix_nonants) on path 6 and
+    on the register path give the same objectives; restoring the bounds restores the LP."""
+    import torch
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd import _lib
+    S = 512
+    b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=1, num_scens=S)
+    e = PHEngine(b, device="cuda:0")
+    e.solve(_lib.default_options(kernel=6, eps_rel=1e-10), warm=False)
+    base = e.host("obj").copy()
+    rng = np.random.default_rng(3)
+    xf = rng.uniform(50.0, 200.0, size=(b.nn, S))  # total acreage <= 500: always feasible
+    xfix = torch.as_tensor(xf, device=e.device)
+    _lib.check(e.lib.phgpu_fix_nonants(e.h, xfix.data_ptr(), None), "fix")
+    got = {}
+    for k in (6, 2):
+        e.solve(_lib.default_options(kernel=k, eps_rel=1e-10), warm=False)
+        assert (e.host("status") == 0).all()
+        got[k] = e.host("obj").copy()
+        assert np.abs(e.host("x")[:, b.nonant_col] - xf.T).max() <= 1e-7
+    assert np.abs(got[6] - got[2]).max() <= OBJ_REL * np.abs(got[2]).max()
+    _lib.check(e.lib.phgpu_fix_nonants(e.h, None, None), "restore")
+    e.solve(_lib.default_options(kernel=6, eps_rel=1e-10), warm=False)
+    assert np.abs(e.host("obj") - base).max() <= 1e-7 * np.abs(base).max()
+    e.close()

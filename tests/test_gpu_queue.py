@@ -40,7 +40,7 @@ def _run(mode, S, iters):
         del os.environ["PHGPU_REG_REC"]
 
 
-def test_record_mode_matches_scenario_order(gpu):
+def test_record_mode_matches_scenario_order(gpu, register_path):
     S = 20000
     a = _run(0, S, 3)
     b = _run(1, S, 3)

@@ -59,9 +59,11 @@ def _run_and_compare(ph, g):
     return tb
 
 
-def test_headline_farmer65536_cm1(gpu):
-    """Config 3 on one GPU: the bench instance, checked end to end (trivial bound,
-    sampled Iter0 objectives, x̄ and conv of 5 PH iterations, sampled W, E[obj])."""
+def test_headline_farmer65536_cm1_register_path(gpu, register_path):
+    """Config 3 on one GPU on the register path (the bench instance until round 3; path 6,
+    the interior point, is tested on the same fixture in test_gpu_ipm.py), checked end to
+    end (trivial bound, sampled Iter0 objectives, x̄ and conv of 5 PH iterations, sampled
+    W, E[obj])."""
     g = SCALE["farmer65536_cm1"]
     names = [f"scen{i}" for i in range(65536)]
     from mpisppy_amd.examples import farmer
@@ -83,7 +85,7 @@ def test_config2_farmer1024_cm10_bound(gpu):
     _run_and_compare(ph, g)
 
 
-def test_headline_instance_on_a_slice(gpu):
+def test_headline_instance_on_a_slice(gpu, register_path):
     """The same L = 4 <3,3,2,4> instance pinned on a 4,096-scenario slice
     (PHGPU_LANES=4): Iter0 objectives of every scenario in the slice."""
     g = SCALE["farmer65536_cm1"]

@@ -64,6 +64,7 @@ def _run(make, spec):
 CASES = {
     "farmer3": lambda spec: _farmer(3, spec, 1e-3),
     "farmer4096_record_mode": lambda spec: _farmer(4096, spec, 3e-2),
+    "farmer4096_ipm": lambda spec: _farmer(4096, spec, 3e-2),
     "farmer256_global_kernel": lambda spec: _farmer(256, spec, 3e-2, kernel=1),
     "aircond432": lambda spec: _aircond(spec, 1e-4),
 }
@@ -72,18 +73,23 @@ CASES = {
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_speculative_solve_is_invisible(gpu, case):
     keep = os.environ.get("PHGPU_REG_REC")
+    keep_ipm = os.environ.get("PHGPU_IPM")
     if case == "farmer4096_record_mode":
         os.environ["PHGPU_REG_REC"] = "1"
+        os.environ["PHGPU_IPM"] = "0"
     try:
         a = _run(CASES[case], True)
         b = _run(CASES[case], False)
     finally:
-        if keep is None:
-            os.environ.pop("PHGPU_REG_REC", None)
-        else:
-            os.environ["PHGPU_REG_REC"] = keep
+        for k, v in (("PHGPU_REG_REC", keep), ("PHGPU_IPM", keep_ipm)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     if case == "farmer4096_record_mode":
         assert a["kernel"]["rec"] == 1, a["kernel"]
+    if case == "farmer4096_ipm":
+        assert a["kernel"]["path"] == 6, a["kernel"]
     assert a["iter"] == b["iter"] and a["conv"] == b["conv"], (a["iter"], b["iter"], a["conv"], b["conv"])
     for k in ("W", "xbar", "node_buf", "x", "x_after", "iters_after"):
         assert np.array_equal(a[k], b[k]), (case, k, np.abs(a[k] - b[k]).max())

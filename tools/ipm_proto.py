@@ -32,7 +32,34 @@ def ruiz(A, iters=10):
     return As, Dr, Dc
 
 
-def ipm(A, c, q, lb, ub, rl, ru, eps=1e-9, max_it=100, x0=None, verbose=False, common_step=True):
+def ldl_factor(M, piv_rel=1e-30):
+    """In-place batched LDL^T without pivoting (the kernel's order); a pivot below
+    piv_rel x the row's original diagonal is replaced by 1e128 (that row's step -> 0)."""
+    S, m, _ = M.shape
+    L = M.copy()
+    d = np.zeros((S, m))
+    dg = np.einsum("smm->sm", M).copy()
+    for k in range(m):
+        dk = L[:, k, k] - (L[:, k, :k] ** 2 * d[:, :k]).sum(1)
+        dk = np.where(dk > piv_rel * np.maximum(dg[:, k], 1e-300), dk, 1e128)
+        d[:, k] = dk
+        for i in range(k + 1, m):
+            L[:, i, k] = (L[:, i, k] - (L[:, i, :k] * L[:, k, :k] * d[:, :k]).sum(1)) / dk
+    return L, d
+
+
+def ldl_solve(L, d, r):
+    S, m = r.shape
+    z = r.copy()
+    for k in range(m):
+        z[:, k] -= (L[:, k, :k] * z[:, :k]).sum(1)
+    z /= d
+    for k in range(m - 1, -1, -1):
+        z[:, k] -= (L[:, k + 1:, k] * z[:, k + 1:]).sum(1)
+    return z
+
+
+def ipm(A, c, q, lb, ub, rl, ru, eps=1e-9, max_it=100, x0=None, verbose=False, common_step=True, regp=1e-12, regd=1e-12, single=None):
     """Vectorised over the leading scenario axis.  Returns x, y, obj, iters, converged."""
     S, m, n = A.shape
     gam = np.maximum(1.0, np.abs(c).max(1))[:, None]
@@ -73,7 +100,6 @@ def ipm(A, c, q, lb, ub, rl, ru, eps=1e-9, max_it=100, x0=None, verbose=False, c
     iters = np.zeros(S, int)
     bnorm = np.sqrt(np.where(np.isfinite(rl), rl, 0) ** 2 + np.where(np.isfinite(ru) & ~eq, ru, 0) ** 2).sum(1)
     cnorm = np.sqrt((c * c).sum(1))
-    reg = 1e-12
     for it in range(max_it):
         sl = np.where(hl, x - L, 1.0)
         su = np.where(hu, U - x, 1.0)
@@ -112,18 +138,20 @@ def ipm(A, c, q, lb, ub, rl, ru, eps=1e-9, max_it=100, x0=None, verbose=False, c
         rp = np.where(eq, Ax - RL, Ax - w)
         Sx = np.where(hl, zl / sl, 0) + np.where(hu, zu / su, 0)
         Sw = np.where(hlw, zlw / slw, 0) + np.where(huw, zuw / suw, 0)
-        Dx = 1.0 / (q + Sx + reg)
-        Einv = np.where(eq, reg, 1.0 / np.where(eq, 1.0, Sw))
+        Dx = 1.0 / (q + Sx + regp)
+        Einv = np.where(eq, regd, 1.0 / np.where(eq, 1.0, Sw) + regd)
         M = np.einsum("smn,sn,skn->smk", A, Dx, A) + Einv[:, :, None] * np.eye(m)[None]
-        M = np.where(done[:, None, None], np.eye(m)[None], M)
+        bad = ~np.isfinite(M).all((1, 2))
+        M = np.where((done | bad)[:, None, None], np.eye(m)[None], M)
+        LF, DF = ldl_factor(M)
 
         def solve(tl, tu, tlw, tuw):
             hx = -rd_ + np.where(hl, tl / sl - zl, 0) - np.where(hu, tu / su - zu, 0)
             hw = -rw + np.where(hlw, tlw / slw - zlw, 0) - np.where(huw, tuw / suw - zuw, 0)
             rhs = -rp - np.einsum("smn,sn->sm", A, Dx * hx) + np.where(eq, 0.0, hw / np.where(eq, 1.0, Sw))
-            dy = np.linalg.solve(M, rhs[..., None])[..., 0]
+            dy = ldl_solve(LF, DF, rhs)
             dx = Dx * (hx + np.einsum("smn,sm->sn", A, dy))
-            dw = np.where(eq, 0.0, (hw - dy) / np.where(eq, 1.0, Sw))
+            dw = np.where(eq, 0.0, np.einsum("smn,sn->sm", A, dx) + rp)   # the primal row equation exactly
             dzl = np.where(hl, (tl - sl * zl - zl * dx) / sl, 0)
             dzu = np.where(hu, (tu - su * zu + zu * dx) / su, 0)
             dzlw = np.where(hlw, (tlw - slw * zlw - zlw * dw) / slw, 0)
@@ -136,28 +164,36 @@ def ipm(A, c, q, lb, ub, rl, ru, eps=1e-9, max_it=100, x0=None, verbose=False, c
             return np.minimum(1.0, r.min(1))
 
         z = np.zeros_like
-        dx, dw, dy, dzl, dzu, dzlw, dzuw = solve(z(sl), z(su), z(slw), z(suw))
-        ap = np.minimum.reduce([maxstep(sl, dx, hl), maxstep(su, -dx, hu), maxstep(slw, dw, hlw), maxstep(suw, -dw, huw)])
-        ad = np.minimum.reduce([maxstep(zl, dzl, hl), maxstep(zu, dzu, hu), maxstep(zlw, dzlw, hlw), maxstep(zuw, dzuw, huw)])
-        if common_step:
+        if single is not None:
+            if it == 0:
+                aprev = np.zeros(S)
+            sig = single(aprev, mu)
+            sm = (sig * mu)[:, None]
+            dx, dw, dy, dzl, dzu, dzlw, dzuw = solve(sm + z(sl), sm + z(su), sm + z(slw), sm + z(suw))
+        else:
+          dx, dw, dy, dzl, dzu, dzlw, dzuw = solve(z(sl), z(su), z(slw), z(suw))
+          ap = np.minimum.reduce([maxstep(sl, dx, hl), maxstep(su, -dx, hu), maxstep(slw, dw, hlw), maxstep(suw, -dw, huw)])
+          ad = np.minimum.reduce([maxstep(zl, dzl, hl), maxstep(zu, dzu, hu), maxstep(zlw, dzlw, hlw), maxstep(zuw, dzuw, huw)])
+          if common_step:
             ap = ad = np.minimum(ap, ad)
-        mua = (np.where(hl, (sl + ap[:, None] * dx) * (zl + ad[:, None] * dzl), 0).sum(1)
+          mua = (np.where(hl, (sl + ap[:, None] * dx) * (zl + ad[:, None] * dzl), 0).sum(1)
                + np.where(hu, (su - ap[:, None] * dx) * (zu + ad[:, None] * dzu), 0).sum(1)
                + np.where(hlw, (slw + ap[:, None] * dw) * (zlw + ad[:, None] * dzlw), 0).sum(1)
                + np.where(huw, (suw - ap[:, None] * dw) * (zuw + ad[:, None] * dzuw), 0).sum(1)) / np.maximum(ncomp, 1)
-        sig = (mua / mu) ** 3
-        sm = (sig * mu)[:, None]
-        tl = sm - dx * dzl
-        tu = sm + dx * dzu
-        tlw = sm - dw * dzlw
-        tuw = sm + dw * dzuw
-        dx, dw, dy, dzl, dzu, dzlw, dzuw = solve(tl, tu, tlw, tuw)
+          sig = np.where(mu > 0, (mua / np.where(mu > 0, mu, 1)) ** 3, 0.0)
+          sm = (sig * mu)[:, None]
+          tl = sm - dx * dzl
+          tu = sm + dx * dzu
+          tlw = sm - dw * dzlw
+          tuw = sm + dw * dzuw
+          dx, dw, dy, dzl, dzu, dzlw, dzuw = solve(tl, tu, tlw, tuw)
         ap = np.minimum.reduce([maxstep(sl, dx, hl), maxstep(su, -dx, hu), maxstep(slw, dw, hlw), maxstep(suw, -dw, huw)])
         ad = np.minimum.reduce([maxstep(zl, dzl, hl), maxstep(zu, dzu, hu), maxstep(zlw, dzlw, hlw), maxstep(zuw, dzuw, huw)])
         if common_step:
             ap = ad = np.minimum(ap, ad)
         if verbose:
             print('   mu', mu[0], 'sig', sig[0], 'ap', ap[0], 'ad', ad[0])
+        aprev = np.minimum(ap, ad)
         ap = np.minimum(1.0, 0.995 * ap)[:, None]
         ad = np.minimum(1.0, 0.995 * ad)[:, None]
         act = ~done[:, None]
