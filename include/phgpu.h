@@ -220,6 +220,14 @@ int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
  * output), counts: device int32[4]. */
 int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_t* counts, void* stream);
 
+/* Statistics of the last solve (phgpu_solve / phgpu_solve_deferred on this handle),
+ * enqueued on stream into out[6] (device or pinned host memory): the number of local
+ * scenarios with status 0..3 (what phgpu_status_counts gives for its status output), the
+ * sum and the maximum of its iters output.  Path 6 accumulates them inside its kernels
+ * (then this is one 48-byte copy); for the other paths a one-block reduction over the
+ * last solve's outputs computes them (iters may have been NULL: sum = max = 0). */
+int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream);
+
 /* Fix the nonants of every local scenario (lb = ub = xfix[k*S + s], original units,
  * clipped to the model bounds) for the following solves, or restore the model bounds
  * when xfix is NULL.  A NaN entry leaves that nonant at its model bounds (partial

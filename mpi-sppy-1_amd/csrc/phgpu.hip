@@ -150,6 +150,12 @@ struct phgpu_state {
     ipm_module* ipm;
     int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity;
     int32_t *ipm_list, *ipm_cnt;
+    // solve statistics (phgpu_solve_stats): path 6 accumulates them in its kernels (by
+    // parity, [2][8]); other paths get them from k_solve_stats over the last solve's
+    // status / iters outputs into stats_gen[8].  last_stats: where the last solve's are
+    // (null: compute on request)
+    unsigned long long *ipm_stats, *stats_gen, *last_stats;
+    const int32_t *last_status, *last_iters;
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -1653,12 +1659,15 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         ALLOC(h->yt, (size_t)m * Sz);
     }
     ALLOC(h->qhead, 1);
+    ALLOC(h->stats_gen, 8);
     if (!h->shared) {  // path 6: the pattern's factor size, the fallback list and its counters
         h->ipm_nf = ipm_nf_bound(n, m, row_ptr, col_idx);
         if (h->ipm_nf > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 4);
-            if (hipMemset(h->ipm_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess) {
+            ALLOC(h->ipm_stats, 16);
+            if (hipMemset(h->ipm_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess ||
+                hipMemset(h->ipm_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
                 phgpu_destroy(h);
                 return set_err(-2, "hipMemset failed");
             }
@@ -2083,6 +2092,9 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     h->wq = defer ? 1 - h->wslot : h->wslot;
     bind_slots(h);
     const int wq = h->wq;
+    h->last_stats = nullptr;  // path 6 sets it when its kernels produce the statistics
+    h->last_status = status;
+    h->last_iters = iters;
     phgpu_options o;
     if (opt) o = *opt;
     else phgpu_default_options(&o);
@@ -2412,6 +2424,46 @@ extern "C" int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_
     return 0;
 }
 
+// statistics of a solve from its outputs: counts by status, iteration sum and maximum
+__global__ void __launch_bounds__(SC_T) k_solve_stats(const int32_t* __restrict__ status,
+                                                     const int32_t* __restrict__ iters, int64_t S,
+                                                     unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long c[6];
+    if (threadIdx.x < 6) c[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long loc[4] = {0, 0, 0, 0}, isum = 0, imax = 0;
+    for (int64_t t = threadIdx.x; t < S; t += SC_T) {
+        const int v = status[t];
+        loc[0] += v == 0, loc[1] += v == 1, loc[2] += v == 2, loc[3] += v == 3;
+        if (iters) {
+            const unsigned long long i = (unsigned long long)iters[t];
+            isum += i;
+            imax = i > imax ? i : imax;
+        }
+    }
+    for (int k = 0; k < 4; ++k)
+        if (loc[k]) atomicAdd(&c[k], loc[k]);
+    if (isum) atomicAdd(&c[4], isum);
+    if (imax) atomicMax(&c[5], imax);
+    __syncthreads();
+    if (threadIdx.x < 6) out[threadIdx.x] = c[threadIdx.x];
+}
+
+extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
+    if (!h || !out) return set_err(-1, "null argument");
+    if (!h->last_status) return set_err(-1, "phgpu_solve_stats: no solve yet");
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned long long* src = h->last_stats;
+    if (!src) {
+        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
+                           h->stats_gen);
+        HIPCHK(hipGetLastError());
+        src = h->stats_gen;
+    }
+    HIPCHK(hipMemcpyAsync(out, src, 6 * sizeof(int64_t), hipMemcpyDefault, st));
+    return 0;
+}
+
 extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* stream) {
     if (!h) return set_err(-1, "null handle");
     if (h->nn == 0) return 0;
@@ -2463,6 +2515,8 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
     }
     if (h->ipm_list) (void)hipFree(h->ipm_list);
     if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
+    if (h->ipm_stats) (void)hipFree(h->ipm_stats);
+    if (h->stats_gen) (void)hipFree(h->stats_gen);
     if (!h->shared) {  // warm-start slot 1 (slot 0 is x / y / omega / sk_iters above)
         void* slot1[] = {h->xs[1], h->ys[1], h->oms[1], h->its_s[1]};
         for (void* p : slot1)

@@ -47,7 +47,7 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_solve", "phgpu_solve_deferred", "phgpu_commit", "phgpu_ph_reduce", "phgpu_ph_update",
            "phgpu_expectations",
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
-           "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source"]
+           "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats"]
 
 _lib = None
 
@@ -87,6 +87,7 @@ def load(path=None):
     lib.phgpu_workspace_bytes.restype = c_i64
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
+    lib.phgpu_solve_stats.argtypes = [c_vp, c_vp, c_vp]
     lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl),
                                      ctypes.c_char_p, ctypes.c_size_t, P_i32]
     for name in EXPORTS:

@@ -198,12 +198,10 @@ class PHEngine:
     # -------------------------------------------------------------- instrumentation
     def instrument(self, max_solves):
         """Record the next ``max_solves`` phgpu_solve launches: HIP events on the launch
-        stream around each launch and a device snapshot of the per-scenario PDHG
-        iteration counts (one D2D copy after the launch, outside the event pair).  Used
-        by bench.py for the per-launch roofline inside its timed region."""
-        self._ins = {"events": [], "iters": torch.empty((max_solves, self.S), dtype=torch.int32,
-                                                         device=self.device),
-                     "counts": torch.zeros((max_solves, 4), dtype=torch.int32, device=self.device),
+        stream around each launch and the launch's statistics (phgpu_solve_stats: status
+        counts, iteration sum and maximum; one 48-byte copy after the launch, outside the
+        event pair).  Used by bench.py for the per-launch roofline inside its timed region."""
+        self._ins = {"events": [], "stats": torch.zeros((max_solves, 6), dtype=torch.int64, device=self.device),
                      "ar_events": []}
 
     def instrumented(self):
@@ -213,7 +211,7 @@ class PHEngine:
             return []
         torch.cuda.synchronize(self.device)
         k = len(ins["events"])
-        its = ins["iters"][:k].sum(dim=1, dtype=torch.int64).cpu().tolist()
+        its = ins["stats"][:k, 4].cpu().tolist()
         return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
 
     def instrumented_not_optimal(self):
@@ -221,7 +219,7 @@ class PHEngine:
         ins = getattr(self, "_ins", None)
         if not ins:
             return []
-        return ins["counts"][:len(ins["events"]), 1:].sum(dim=1).cpu().tolist()
+        return ins["stats"][:len(ins["events"]), 1:4].sum(dim=1).cpu().tolist()
 
     def instrumented_allreduce_ms(self):
         """Total ms of the x̄ / conv all-reduces issued while instrumenting (HIP events on
@@ -235,7 +233,7 @@ class PHEngine:
     def _allreduce_sum_(self, t):
         """comm.allreduce_sum_ with HIP events around it while instrumenting."""
         ins = getattr(self, "_ins", None)
-        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["iters"].shape[0]:
+        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["stats"].shape[0]:
             return self.comm.allreduce_sum_(t)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
@@ -262,7 +260,7 @@ class PHEngine:
         else:
             out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
-        rec = ins is not None and len(ins["events"]) < ins["iters"].shape[0]
+        rec = ins is not None and len(ins["events"]) < ins["stats"].shape[0]
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -274,11 +272,10 @@ class PHEngine:
         if rec:
             ev[1].record()
             k = len(ins["events"])
-            ins["iters"][k].copy_(out["iters"])
-            # status counts of this launch by the library's one-block reduction (a torch
-            # reduction here stalls the host ~2 ms per call)
-            _lib.check(self.lib.phgpu_status_counts(self.h, _ptr(out["status"]), _ptr(ins["counts"][k]),
-                                                    self._stream()), "phgpu_status_counts")
+            # the launch's statistics (path 6 counts them in its kernels; a torch reduction
+            # here would stall the host ~2 ms per call)
+            _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(ins["stats"][k]), self._stream()),
+                       "phgpu_solve_stats")
             ins["events"].append(ev)
             ins.setdefault("spec", []).append(speculative)
 
@@ -306,16 +303,19 @@ class PHEngine:
         return int(c[1:].sum())
 
     def count_not_optimal_async(self):
-        """Start the same count without waiting: the counts go to pinned host memory
+        """The same count for the solve just launched, without waiting: its statistics
+        (phgpu_solve_stats, accumulated in the path-6 kernels) go to pinned host memory
         behind an event; ``pending_not_optimal`` reads them (free after the next host
         synchronisation)."""
-        self._status_counts()
-        self._counts_host.copy_(self._counts_dev, non_blocking=True)
-        self._counts_ev.record()
+        if not hasattr(self, "_stats_host"):
+            self._stats_host = torch.zeros(6, dtype=torch.int64).pin_memory()
+            self._stats_ev = torch.cuda.Event()
+        _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(self._stats_host), self._stream()), "phgpu_solve_stats")
+        self._stats_ev.record()
 
     def pending_not_optimal(self):
-        self._counts_ev.synchronize()
-        return int(self._counts_host[1:].sum())
+        self._stats_ev.synchronize()
+        return int(self._stats_host[1:4].sum())
 
     def compute_xbar_partials(self):
         _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),

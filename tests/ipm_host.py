@@ -29,6 +29,11 @@ struct ipm_dim3 { unsigned x, y, z; };
 static ipm_dim3 blockIdx, threadIdx, blockDim;
 #define __builtin_amdgcn_rcp(x) (1.0 / (x))
 static inline int atomicAdd(int* p, int v) { int o = *p; *p += v; return o; }
+static inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) { unsigned long long o = *p; *p += v; return o; }
+static inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) { unsigned long long o = *p; if (v > o) *p = v; return o; }
+static inline unsigned long long __ballot(bool b) { return b ? 1ull : 0ull; }
+static inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+template <class T> static inline T __shfl_xor(T, int, int) { return T(0); }  // one lane: the others contribute 0
 """
 
 DRIVER = r"""
@@ -73,7 +78,7 @@ class _Params(ctypes.Structure):
                                   "status", "iters", "fail_list", "fail_n", "fail_zero", "qhead_zero")]
                 + [("S", ctypes.c_longlong), ("W_on", ctypes.c_int), ("prox_on", ctypes.c_int),
                    ("eps_rel", ctypes.c_double), ("eps_abs", ctypes.c_double), ("eps_tight", ctypes.c_double),
-                   ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP)])
+                   ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP)])
 
 
 def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13):
@@ -118,6 +123,9 @@ def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_i
     p.S, p.W_on, p.prox_on = S, int(W is not None), int(rho is not None)
     p.eps_rel, p.eps_abs, p.max_ipm, p.eps_tight = eps_rel, eps_abs, max_ipm, eps_tight
     p.x_in, p.y_in = None, None
+    st16 = np.zeros(16, dtype=np.uint64)
+    keep.append(st16)
+    p.stats, p.stats_zero = st16.ctypes.data, st16[8:].ctypes.data
     lib.ipm_run(ctypes.byref(p), S)
     st = status.copy()
     st[fl[:cnt[0]]] = -1

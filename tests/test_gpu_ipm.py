@@ -173,3 +173,30 @@ def test_path6_fixed_nonants_match_register_path(gpu):
     e.solve(_lib.default_options(kernel=6, eps_rel=1e-10), warm=False)
     assert np.abs(e.host("obj") - base).max() <= 1e-7 * np.abs(base).max()
     e.close()
+
+
+@pytest.mark.parametrize("kernel,maxit", [(6, None), (6, "3"), (2, None)])
+def test_solve_stats_match_the_outputs(gpu, kernel, maxit):
+    """phgpu_solve_stats: path 6 accumulates the statistics in its kernels (IPM and
+    fallback), the other paths reduce the outputs; both equal the host counts."""
+    import torch
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd import _lib
+    S = 3000
+    b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=1, num_scens=S)
+    e = PHEngine(b, device="cuda:0")
+    if maxit:
+        os.environ["PHGPU_IPM_MAXIT"] = maxit
+    try:
+        for warm in (False, True):
+            e.solve(_lib.default_options(kernel=kernel), warm=warm)
+            out = torch.zeros(6, dtype=torch.int64, device=e.device)
+            _lib.check(e.lib.phgpu_solve_stats(e.h, out.data_ptr(), None), "stats")
+            got = out.cpu().numpy()
+            st, it = e.host("status"), e.host("iters")
+            want = [int((st == k).sum()) for k in range(4)] + [int(it.sum()), int(it.max())]
+            assert list(got) == want, (list(got), want)
+    finally:
+        os.environ.pop("PHGPU_IPM_MAXIT", None)
+    e.close()
