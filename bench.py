@@ -242,7 +242,7 @@ def ipm_flops_per_iter(b, ipm):
             + 8 * sides + 6 * sides + 2 * n + 4 * m)
 
 
-def roofline_ipm(b, ipm, launches, ws_bytes):
+def roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir):
     """Roofline of the interior-point kernel (path 6): fp64 issue-bound like the other
     register-resident paths (each lane holds its scenario's whole IPM state), achieved =
     ipm_flops_per_iter x IPM iterations per launch / mean HIP-event launch time."""
@@ -250,10 +250,24 @@ def roofline_ipm(b, ipm, launches, ws_bytes):
     units = float(np.mean([u for _, u in launches]))
     F = ipm_flops_per_iter(b, ipm)
     tflops = F * units / (launch_ms * 1e-3) / 1e12
+    kname = "k_solve_ipm" if int(ipm.get("lanes", 1)) <= 1 else "k_solve_ipm_ml"
+    traffic, src = None, None
+    pmc = _latest_profile_file(f"pmc_summary_{tag}.json", pdir)
+    if pmc:
+        try:
+            tr = json.load(open(pmc)).get("solve_traffic_bytes_per_launch", {}).get(kname)
+            if tr is not None:
+                traffic, src = tr["total_upper"], os.path.relpath(pmc, ROOT)
+        except Exception:
+            traffic = None
+    hbm_gbs = traffic / (launch_ms * 1e-3) / 1e9 if traffic else None
     return {"bound": "fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "traffic_source": None,
+            "frac": tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": src,
+            "hbm": {"achieved_GBs": hbm_gbs, "peak_GBs": HBM_PEAK_GBS,
+                    "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
+                    "note": "measured PMC bytes per launch (profiles/) / HIP-event launch time"},
             "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
-            "kernel": "k_solve_ipm (hipRTC, pattern-specialised)", "lanes_per_scenario": 1,
+            "kernel": kname + " (hipRTC, pattern-specialised)", "lanes_per_scenario": int(ipm.get("lanes", 1)),
             "launch_ms": launch_ms, "scenario_iters_per_launch": units, "flops_per_scenario_iter": F,
             "ipm": {k: ipm[k] for k in ("rows", "factor_entries", "scratch_bytes", "compile_s")},
             "note": ("achieved = F x IPM scenario-iterations per launch / mean HIP-event launch time (the "
@@ -283,7 +297,7 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir, ipm=None):
     elif path == 4:
         return roofline_stream(b, launches, ws_bytes, tag, pdir)
     elif path == 6:
-        return roofline_ipm(b, ipm, launches, ws_bytes)
+        return roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir)
     else:
         kname, lanes = "k_solve", 1
     launch_ms = float(np.mean([t for t, _ in launches]))

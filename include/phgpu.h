@@ -257,24 +257,27 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
-/* Path-6 (interior point) diagnostics: info[10] = {1 if path 6 applies to the pattern,
+/* Path-6 (interior point) diagnostics: info[11] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
  * (path 6 is then not the automatic path), 1 if a module is compiled, rows in its normal
  * equations, its factor entries, its scratch bytes per lane, its hipRTC compile seconds,
- * flops of one LDL' factorisation, flops of one forward + backward solve}. */
+ * flops of one LDL' factorisation, flops of one forward + backward solve, lanes per
+ * scenario of its IPM kernel (1, or a lane group of 2..16: more lanes for fewer local
+ * scenarios, PHGPU_IPM_LANES pins it)}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
 /* The path-6 source the library generates for a pattern and its data flags (host code
  * only; tests and tools).  flags / v0 are per element of [A nnz | c n | q n | lb n | ub n |
  * rl m | ru m]: bit 0 the same value in every scenario, bit 1 finite in some scenario,
  * bit 2 finite in every scenario, bit 3 (rl elements) rl == ru in every scenario; v0 the
- * first scenario's value.  nonant_slot[n]: nonant index of each column or -1.  Writes the
+ * first scenario's value.  nonant_slot[n]: nonant index of each column or -1; lanes: lanes
+ * per scenario of the IPM kernel (1, 2, 4, 8 or 16).  Writes the
  * NUL-terminated source to buf when len exceeds its length; returns the length + 1 (or a
  * negative error); info[4] (may be NULL) = {rows in the normal equations, factor entries,
  * factorisation flops, solve flops}. */
 int phgpu_ipm_source(int32_t n, int32_t m, int32_t nnz, const int32_t* row_ptr, const int32_t* col_idx,
-                     const int32_t* nonant_slot, const int32_t* flags, const double* v0, char* buf, size_t len,
-                     int32_t* info);
+                     const int32_t* nonant_slot, const int32_t* flags, const double* v0, int32_t lanes, char* buf,
+                     size_t len, int32_t* info);
 
 #ifdef __cplusplus
 }

@@ -148,7 +148,7 @@ struct phgpu_state {
     // (0: not eligible); 1 once a compiled module spilled (path 6 is then not the
     // default); the fallback list [S] and its counters {fail_n[2], qhead[2]} by parity
     ipm_module* ipm;
-    int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity;
+    int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity, ipm_spill1;
     int32_t *ipm_list, *ipm_cnt;
     // solve statistics (phgpu_solve_stats): path 6 accumulates them in its kernels (by
     // parity, [2][8]); other paths get them from k_solve_stats over the last solve's
@@ -1664,9 +1664,9 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         h->ipm_nf = ipm_nf_bound(n, m, row_ptr, col_idx);
         if (h->ipm_nf > 0) {
             ALLOC(h->ipm_list, Sz);
-            ALLOC(h->ipm_cnt, 4);
+            ALLOC(h->ipm_cnt, 6);
             ALLOC(h->ipm_stats, 16);
-            if (hipMemset(h->ipm_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess ||
+            if (hipMemset(h->ipm_cnt, 0, 6 * sizeof(int32_t)) != hipSuccess ||
                 hipMemset(h->ipm_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
                 phgpu_destroy(h);
                 return set_err(-2, "hipMemset failed");
@@ -2572,7 +2572,7 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     if (!h || !info) return set_err(-1, "null argument");
-    for (int k = 0; k < 10; ++k) info[k] = 0.0;
+    for (int k = 0; k < 11; ++k) info[k] = 0.0;
     info[0] = ipm_eligible(h) ? 1.0 : 0.0;
     info[1] = h->ipm_nf;
     info[2] = h->ipm_off;
@@ -2584,6 +2584,7 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
         info[7] = h->ipm->compile_s;
         info[8] = h->ipm->fac_flops;
         info[9] = h->ipm->sol_flops;
+        info[10] = h->ipm->L;
     }
     return 0;
 }

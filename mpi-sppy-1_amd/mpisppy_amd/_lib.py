@@ -88,7 +88,7 @@ def load(path=None):
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
     lib.phgpu_solve_stats.argtypes = [c_vp, c_vp, c_vp]
-    lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl),
+    lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl), c_i32,
                                      ctypes.c_char_p, ctypes.c_size_t, P_i32]
     for name in EXPORTS:
         if name != "phgpu_workspace_bytes":
@@ -134,7 +134,7 @@ def ipm_flags(batch):
     return np.concatenate(flags).astype(np.int32), np.concatenate(v0).astype(np.float64)
 
 
-def ipm_source(batch):
+def ipm_source(batch, lanes=1):
     """The path-6 source the library generates for a batch (no GPU): (text, (rows, factor
     entries, factorisation flops, solve flops))."""
     import numpy as np
@@ -147,7 +147,7 @@ def ipm_source(batch):
     ip = lambda a: a.ctypes.data_as(P_i32)  # noqa: E731
     info = np.zeros(4, dtype=np.int32)
     args = (batch.n, batch.m, batch.nnz, ip(rp), ip(ci), ip(slot), ip(flags),
-            v0.ctypes.data_as(ctypes.POINTER(c_dbl)))
+            v0.ctypes.data_as(ctypes.POINTER(c_dbl)), lanes)
     need = lib.phgpu_ipm_source(*args, None, 0, ip(info))
     if need < 0:
         raise PhgpuError(f"phgpu_ipm_source failed: {last_error()}")

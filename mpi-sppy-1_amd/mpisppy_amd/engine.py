@@ -165,10 +165,10 @@ class PHEngine:
 
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
-        info = (ctypes.c_double * 10)()
+        info = (ctypes.c_double * 11)()
         _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
         keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
-                "factor_flops", "solve_flops"]
+                "factor_flops", "solve_flops", "lanes"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state

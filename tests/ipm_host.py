@@ -75,7 +75,7 @@ _VP = ctypes.c_void_p
 class _Params(ctypes.Structure):
     _fields_ = ([(f, _VP) for f in ("A", "c", "q", "lb", "ub", "rl", "ru", "objc", "lbh", "ubh", "Dc", "Dr", "W", "rho",
                                   "xbar", "omega_in", "omega_out", "x_w", "y_w", "xout", "yout", "obj", "bound",
-                                  "status", "iters", "fail_list", "fail_n", "fail_zero", "qhead_zero")]
+                                  "status", "iters", "fail_list", "fail_n", "zero3")]
                 + [("S", ctypes.c_longlong), ("W_on", ctypes.c_int), ("prox_on", ctypes.c_int),
                    ("eps_rel", ctypes.c_double), ("eps_abs", ctypes.c_double), ("eps_tight", ctypes.c_double),
                    ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP)])
@@ -117,8 +117,7 @@ def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_i
     p.omega_in, p.omega_out = ptr(np.ones(S)), ptr(omo)
     p.x_w, p.y_w, p.xout, p.yout = ptr(out["xw"]), ptr(out["yw"]), ptr(out["x"]), ptr(out["y"])
     p.obj, p.bound, p.status, p.iters = ptr(obj), ptr(bound), ptr(status), ptr(iters)
-    p.fail_list, p.fail_n, p.fail_zero, p.qhead_zero = (ptr(fl), cnt[0:].ctypes.data, cnt[1:].ctypes.data,
-                                                        cnt[3:].ctypes.data)
+    p.fail_list, p.fail_n, p.zero3 = ptr(fl), cnt[0:].ctypes.data, cnt[1:].ctypes.data
     keep.append(cnt)
     p.S, p.W_on, p.prox_on = S, int(W is not None), int(rho is not None)
     p.eps_rel, p.eps_abs, p.max_ipm, p.eps_tight = eps_rel, eps_abs, max_ipm, eps_tight

@@ -200,3 +200,82 @@ def test_solve_stats_match_the_outputs(gpu, kernel, maxit):
     finally:
         os.environ.pop("PHGPU_IPM_MAXIT", None)
     e.close()
+
+
+# ---------------------------------------------------------------- lane groups (ML_L > 1)
+@pytest.fixture
+def ipm_lanes(request):
+    keep = os.environ.get("PHGPU_IPM_LANES")
+    os.environ["PHGPU_IPM_LANES"] = str(request.param)
+    yield request.param
+    if keep is None:
+        os.environ.pop("PHGPU_IPM_LANES", None)
+    else:
+        os.environ["PHGPU_IPM_LANES"] = keep
+
+
+@pytest.mark.parametrize("ipm_lanes", [2, 4, 8, 16], indirect=True)
+def test_lane_groups_farmer_slice_vs_fixture(gpu, ipm_lanes):
+    """The multi-lane kernel (k_solve_ipm_ml) on config 3's fixture slice: Iter0 objectives,
+    then 5 PH iterations against the same run on one lane per scenario (x̄ / W 1e-5)."""
+    g = SCALE["farmer65536_cm1"]
+    names = [f"scen{i}" for i in range(0, 65536, 16)]
+    ph = _farmer_ph(names, 1, len(names))
+    ph.PH_Prep()
+    ph.Iter0()
+    ii = ph.engine.ipm_info()
+    assert ii["lanes"] == ipm_lanes and ii["compiled"] == 1, ii
+    st, obj = ph.engine.host("status"), ph.engine.host("obj")
+    assert (st == 0).all()
+    idx = [k for k, s in enumerate(range(0, 65536, 16)) if s in set(g["sample"])]
+    want = np.array([g["iter0_obj"][g["sample"].index(s)] for s in range(0, 65536, 16) if s in set(g["sample"])])
+    assert np.abs(obj[idx] - want).max() <= OBJ_REL * np.abs(want).max()
+    got = _five_iters(ph)
+    os.environ["PHGPU_IPM_LANES"] = "1"
+    ph1 = _farmer_ph(names, 1, len(names))
+    ph1.PH_Prep()
+    ph1.Iter0()
+    assert ph1.engine.ipm_info()["lanes"] == 1
+    ref = _five_iters(ph1)
+    for k in ("xbar", "W"):
+        assert np.abs(got[k] - ref[k]).max() <= ABS, (k, np.abs(got[k] - ref[k]).max())
+    assert np.abs(got["conv"] - ref["conv"]).max() <= ABS
+
+
+def _five_iters(ph):
+    convs = []
+    for _ in range(5):
+        ph.Compute_Xbar()
+        ph.Update_W()
+        convs.append(ph.convergence_diff())
+        ph.solve_loop(solver_options=ph.iterk_solver_options, gripe=True)
+        assert (ph.engine.host("status") == 0).all()
+    return {"xbar": ph.xbar_by_node()["ROOT"][:3].copy(), "W": ph.W_array().copy(), "conv": np.array(convs)}
+
+
+@pytest.mark.parametrize("ipm_lanes", [4, 8], indirect=True)
+def test_lane_groups_aircond432(gpu, ipm_lanes):
+    from mpisppy_amd.examples import aircond
+    from mpisppy_amd.sputils import create_nodenames_from_branching_factors
+    g = GOLD["aircond432_rho1"]
+    kw = dict(g["kwargs"])
+    kw["branching_factors"] = g["branching_factors"]
+    nodes = create_nodenames_from_branching_factors(g["branching_factors"])
+    ph = _ph(g["names"], aircond.scenario_creator, kw, iters=5, all_nodenames=nodes,
+             batch_creator=aircond.batch_creator, iter0_solver_options=dict(K6), iterk_solver_options=dict(K6))
+    conv, eobj, tb = ph.ph_main()
+    assert ph.engine.ipm_info()["lanes"] == ipm_lanes
+    assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
+    assert np.abs(ph.W_array() - np.array(g["traj5"][4]["W"])).max() <= ABS
+
+
+@pytest.mark.parametrize("ipm_lanes", [4], indirect=True)
+@pytest.mark.parametrize("S,with_q", [(67, False), (130, True)])
+def test_lane_groups_random_batches(gpu, ipm_lanes, S, with_q):
+    test_random_batches_on_path6(gpu, S, with_q)
+
+
+@pytest.mark.parametrize("ipm_lanes", [8], indirect=True)
+@pytest.mark.parametrize("kind,code", [("primal", 2), ("dual", 3)])
+def test_lane_groups_hand_infeasible_scenarios_to_the_pdhg(gpu, ipm_lanes, kind, code):
+    test_path6_hands_infeasible_scenarios_to_the_pdhg(gpu, kind, code)
