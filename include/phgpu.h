@@ -204,6 +204,16 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
                     double* W, const double* rho, int update_W, double* conv_local,
                     void* stream);
 
+/* phgpu_ph_update, plus: stats_out (int64[6], may be NULL) receives the statistics of
+ * the handle's last solve launch as phgpu_solve_stats reports them, written by the same
+ * kernel that writes conv_local.  conv_local and stats_out may be host-mapped pinned
+ * memory (zero-copy: the host reads them after an event recorded behind this call),
+ * which saves the copy launches of the PH loop's convergence and gripe readbacks
+ * (phbase.py:330-343, spopt.py:284-294).  Clears no other state. */
+int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double* node_buf, double* xbar,
+                       double* W, const double* rho, int update_W, double* conv_local,
+                       int64_t* stats_out, void* stream);
+
 /* Local probability-weighted sums (spopt.py:310-439) into out[5]:
  *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
  *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s feasible} prob_s, where feasible

@@ -92,6 +92,10 @@ struct phgpu_state {
         pk_XB;
     int last_path;       // path of the last solve (whose layout holds the warm start)
     int scen_set;
+    // 1 if some wave of local scenarios spans two nodes at a nonant's depth (its x̄
+    // contributions go to node_buf by atomics, so node_buf is cleared by a memset first);
+    // 0 if none does (k_xbar_partial clears node_buf itself); -1 not yet known
+    int xbar_mixed;
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
     int occ_cache[8];  // workgroups per CU of each solve kernel (0 = not queried yet)
@@ -867,12 +871,16 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 // each nonant; a wave whose scenarios share one node at that depth writes one
 // partial (deterministic); a mixed wave adds per lane with fp64 atomics.
 __global__ void __launch_bounds__(BLOCK)
-k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf) {
+k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf, int clear) {
     const int64_t S = st.S;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t wave = s / WAVE;
     const bool act = s < S;
     const int half = st.num_nodes * st.nlen_max;
+    // no wave spans two nodes (st.xbar_mixed == 0): this kernel does not touch node_buf
+    // below, so it clears it for k_xbar_final (one launch less than a memset)
+    if (clear)
+        for (int64_t i = s; i < 2 * (int64_t)half; i += (int64_t)gridDim.x * blockDim.x) node_buf[i] = 0.0;
     for (int k = 0; k < st.nn; ++k) {
         const int d = st.nonant_depth[k];
         const int gnode = act ? st.node_of[IX(d)] : -1;
@@ -897,6 +905,22 @@ k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict_
             if ((threadIdx.x & (WAVE - 1)) == 0) st.part_node[wave * st.nn + k] = -1;
         }
     }
+}
+
+// out[0] |= 1 if some wave of local scenarios spans two nodes at a nonant's depth (the
+// test k_xbar_partial makes per wave)
+__global__ void __launch_bounds__(BLOCK) k_xbar_mixed(phgpu_state st, int32_t* __restrict__ out) {
+    const int64_t S = st.S;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = s < S;
+    bool mixed = false;
+    for (int k = 0; k < st.nn; ++k) {
+        const int d = st.nonant_depth[k];
+        const int gnode = act ? st.node_of[IX(d)] : -1;
+        const int g0 = __shfl(gnode, 0, WAVE);
+        mixed |= __any(act && gnode != g0) != 0;
+    }
+    if (mixed && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(out, 1);
 }
 
 // Ordered segmented sum of the per-wave partials, one block per nonant.  The local
@@ -1081,10 +1105,15 @@ k_fix_nonants(phgpu_state st, const double* __restrict__ xfix) {
 }
 
 // Deterministic ordered sum of K interleaved per-wave partials: out[k] = sum_w part[w*K+k].
+// With stats_src / stats_dst (phgpu_ph_update_ex) block 0 also copies a solve's six
+// statistics (a store to host memory here saves a copy launch per PH iteration).
 __global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__ part, int64_t nw, int K,
-                                                     double scale, double* __restrict__ out) {
+                                                     double scale, double* __restrict__ out,
+                                                     const unsigned long long* __restrict__ stats_src = nullptr,
+                                                     int64_t* __restrict__ stats_dst = nullptr) {
     __shared__ double sh[256];
     const int k = blockIdx.x;
+    if (stats_dst && k == 0 && threadIdx.x < 6) stats_dst[threadIdx.x] = (int64_t)stats_src[threadIdx.x];
     double a = 0.0;
     for (int64_t w = threadIdx.x; w < nw; w += 256) a += part[w * K + k];
     sh[threadIdx.x] = a;
@@ -1566,6 +1595,7 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     h->num_nodes = num_nodes;
     h->nlen_max = nlen_max;
     h->nwaves = (S + WAVE - 1) / WAVE;
+    h->xbar_mixed = -1;
     // transposed pattern (host)
     int32_t* cptr = new int32_t[n + 1]();
     int32_t* ridx = new int32_t[nnz > 0 ? nnz : 1];
@@ -1879,6 +1909,7 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
     HIPCHK(cp(h->prob, prob, Sz));
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    h->xbar_mixed = -1;
     const int big = std::max(nnz, std::max(n, m));
     const dim3 gb((unsigned)((big + 255) / 256)), gn((unsigned)((n + 255) / 256)), gm((unsigned)((m + 255) / 256));
     const dim3 gz((unsigned)((nnz + 255) / 256 > 0 ? (nnz + 255) / 256 : 1));
@@ -2013,6 +2044,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     HIPCHK(cp(h->prob, prob, Sz));
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    h->xbar_mixed = -1;
     h->wslot = h->wq = 0;
     h->pending = -1;
     h->have_s[0] = h->have_s[1] = 0;
@@ -2341,47 +2373,6 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     return 0;
 }
 
-extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
-    if (!h || !x || !node_buf) return set_err(-1, "null argument");
-    hipStream_t st = (hipStream_t)stream;
-    const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
-    HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
-    if (h->nn == 0) return 0;
-    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf);
-    HIPCHK(hipGetLastError());
-    return 0;
-}
-
-extern "C" int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf,
-                               double* xbar, double* W, const double* rho, int update_W,
-                               double* conv_local, void* stream) {
-    if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
-        return set_err(-1, "null argument");
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_ph_update, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, xbar, W, rho,
-                       update_W ? 1 : 0);
-    HIPCHK(hipGetLastError());
-    const double scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
-    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)h->part, h->nwaves, 1,
-                       scale, conv_local);
-    HIPCHK(hipGetLastError());
-    return 0;
-}
-
-extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
-                                  const int32_t* status, double* out, void* stream) {
-    if (!h || !obj || !bound || !status || !out) return set_err(-1, "null argument");
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_expect_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, obj, bound, status);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_sum_partials, dim3(5), dim3(256), 0, st, (const double*)h->part, h->nwaves, 5, 1.0,
-                       out);
-    HIPCHK(hipGetLastError());
-    return 0;
-}
-
 // counts[c] = number of local scenarios with status c (c = 0..3), one block
 // counts[k] = #{s : status[s] == k}: one block, four statuses per load, several loads in
 // flight per thread (a device-wide "last block" reduction needs a release fence, i.e. an
@@ -2461,6 +2452,74 @@ extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
         src = h->stats_gen;
     }
     HIPCHK(hipMemcpyAsync(out, src, 6 * sizeof(int64_t), hipMemcpyDefault, st));
+    return 0;
+}
+
+extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
+    if (!h || !x || !node_buf) return set_err(-1, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
+    if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
+                               ? 0 : set_err(-2, "hipMemsetAsync failed");
+    if (h->xbar_mixed < 0) {  // once per scenario data: does any wave span two nodes?
+        int32_t* d = nullptr;
+        int32_t v = 0;
+        HIPCHK(hipMalloc((void**)&d, sizeof(int32_t)));
+        HIPCHK(hipMemsetAsync(d, 0, sizeof(int32_t), st));
+        hipLaunchKernelGGL(k_xbar_mixed, grid_for(h->S), dim3(BLOCK), 0, st, *h, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&v, d, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipFree(d));
+        h->xbar_mixed = v ? 1 : 0;
+    }
+    if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
+    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double* node_buf,
+                                  double* xbar, double* W, const double* rho, int update_W,
+                                  double* conv_local, int64_t* stats_out, void* stream) {
+    if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
+        return set_err(-1, "null argument");
+    if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_update_ex: stats_out before any solve");
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned long long* src = stats_out ? h->last_stats : nullptr;
+    if (stats_out && !src) {  // a path without in-kernel statistics
+        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
+                           h->stats_gen);
+        HIPCHK(hipGetLastError());
+        src = h->stats_gen;
+    }
+    hipLaunchKernelGGL(k_ph_update, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, xbar, W, rho,
+                       update_W ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    const double scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)h->part, h->nwaves, 1,
+                       scale, conv_local, src, stats_out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf,
+                               double* xbar, double* W, const double* rho, int update_W,
+                               double* conv_local, void* stream) {
+    return phgpu_ph_update_ex(h, x, node_buf, xbar, W, rho, update_W, conv_local, nullptr, stream);
+}
+
+extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
+                                  const int32_t* status, double* out, void* stream) {
+    if (!h || !obj || !bound || !status || !out) return set_err(-1, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_expect_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, obj, bound, status);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_sum_partials, dim3(5), dim3(256), 0, st, (const double*)h->part, h->nwaves, 5, 1.0,
+                       out);
+    HIPCHK(hipGetLastError());
     return 0;
 }
 

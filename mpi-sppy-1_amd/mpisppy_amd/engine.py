@@ -123,6 +123,23 @@ class PHEngine:
         # row duals are an optional phgpu_solve output: PH never reads them, so the hot
         # loop leaves them on the device side (set True to have ``y`` filled by solves)
         self.want_duals = False
+        # Host-mapped readbacks (phgpu_ph_update_ex writes conv and the last solve's
+        # statistics straight into pinned host memory, no copy launches): launch ids of the
+        # last solve launch, of the solve whose outputs are current and of a pending
+        # speculative one; row_of maps a launch id to the stats row an update wrote for it.
+        self._launch_id = self._cur_id = self._spec_id = 0
+        self._gripe_id = 0
+        self._row_of = {}
+        self._stats_rows = torch.zeros((1, 6), dtype=torch.int64).pin_memory()
+        self._stats_tmp = torch.zeros(6, dtype=torch.int64).pin_memory()
+        self._conv_host = torch.zeros(1, dtype=torch.float64).pin_memory()
+        self._conv_zero_copy = False
+        # markers: the event behind each update (by update number), recorded lazily -- every
+        # event record is a barrier packet that idles the GPU ~5 us, so one PH step records
+        # one (the instrumented bench shares it with its solve-start timing event)
+        self._upd_seq = 0
+        self._upd_marks = {}
+        self._conv_ev = None
         self._upload()
 
     # -------------------------------------------------------------- plumbing
@@ -201,25 +218,59 @@ class PHEngine:
         stream around each launch and the launch's statistics (phgpu_solve_stats: status
         counts, iteration sum and maximum; one 48-byte copy after the launch, outside the
         event pair).  Used by bench.py for the per-launch roofline inside its timed region."""
-        self._ins = {"events": [], "stats": torch.zeros((max_solves, 6), dtype=torch.int64, device=self.device),
-                     "ar_events": []}
+        self._ins = {"events": [], "ids": [], "max": int(max_solves), "ar_events": [],
+                     "rows": torch.zeros((max_solves + 4, 6), dtype=torch.int64).pin_memory(), "next": 0}
 
     def instrumented(self):
         """[(launch ms, scenario-iterations)] of the recorded launches (syncs)."""
+        return [(a.elapsed_time(b), int(st[4])) for (a, b), st in self._ins_stats()]
+
+    def instrumented_not_optimal(self):
+        """Scenarios not OPTIMAL in each recorded launch."""
+        return [int(st[1:4].sum()) for _, st in self._ins_stats()]
+
+    def _ins_stats(self):
+        """[(event pair, stats[6])] of the recorded launches whose statistics are known: the
+        update after a launch wrote them (phgpu_ph_update_ex), or the launch is the last
+        one (phgpu_solve_stats).  Synchronises."""
         ins = getattr(self, "_ins", None)
         if not ins:
             return []
         torch.cuda.synchronize(self.device)
-        k = len(ins["events"])
-        its = ins["stats"][:k, 4].cpu().tolist()
-        return [(a.elapsed_time(b), int(u)) for (a, b), u in zip(ins["events"], its)]
+        out = []
+        for ev, lid in zip(ins["events"], ins["ids"]):
+            st = self._stats_of(lid)
+            if st is not None:
+                out.append((ev, st))
+        return out
 
-    def instrumented_not_optimal(self):
-        """Scenarios not OPTIMAL in each recorded launch."""
+    def _recording(self):
         ins = getattr(self, "_ins", None)
-        if not ins:
-            return []
-        return ins["stats"][:len(ins["events"]), 1:4].sum(dim=1).cpu().tolist()
+        return ins is not None and len(ins["events"]) < ins["max"]
+
+    def _marker(self, seq=None):
+        """The event behind update ``seq`` (default: the last one), recorded now if it has
+        none yet (then it also covers whatever was queued since)."""
+        seq = self._upd_seq if seq is None else seq
+        ev = self._upd_marks.get(seq)
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._upd_marks[seq] = ev
+        return ev
+
+    def _stats_of(self, lid):
+        """Statistics of launch ``lid`` (host int64[6] copy) or None if no longer known."""
+        where = self._row_of.get(lid)
+        if where is not None:
+            rows, r, seq = where
+            self._marker(seq).synchronize()
+            return rows[r].clone()
+        if lid == self._launch_id and lid:
+            _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(self._stats_tmp), self._stream()), "phgpu_solve_stats")
+            torch.cuda.current_stream(self.device).synchronize()
+            return self._stats_tmp.clone()
+        return None
 
     def instrumented_allreduce_ms(self):
         """Total ms of the x̄ / conv all-reduces issued while instrumenting (HIP events on
@@ -233,7 +284,7 @@ class PHEngine:
     def _allreduce_sum_(self, t):
         """comm.allreduce_sum_ with HIP events around it while instrumenting."""
         ins = getattr(self, "_ins", None)
-        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["stats"].shape[0]:
+        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["max"]:
             return self.comm.allreduce_sum_(t)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
@@ -260,10 +311,17 @@ class PHEngine:
         else:
             out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
-        rec = ins is not None and len(ins["events"]) < ins["stats"].shape[0]
+        rec = self._recording()
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+            if self._upd_seq and self._upd_marks.get(self._upd_seq) is None:
+                self._upd_marks[self._upd_seq] = ev[0]   # the update's marker, shared
+        self._launch_id += 1
+        if speculative:
+            self._spec_id = self._launch_id
+        else:
+            self._cur_id = self._launch_id
         fn = self.lib.phgpu_solve_deferred if speculative else self.lib.phgpu_solve
         _lib.check(fn(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
                       _ptr(out["y"] if self.want_duals else None), _ptr(out["obj"]), _ptr(out["bound"]),
@@ -271,13 +329,10 @@ class PHEngine:
                    "phgpu_solve_deferred" if speculative else "phgpu_solve")
         if rec:
             ev[1].record()
-            k = len(ins["events"])
-            # the launch's statistics (path 6 counts them in its kernels; a torch reduction
-            # here would stall the host ~2 ms per call)
-            _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(ins["stats"][k]), self._stream()),
-                       "phgpu_solve_stats")
+            # the launch's statistics come with the next update (phgpu_ph_update_ex), the
+            # last launch's from phgpu_solve_stats after the loop: no copy per launch
             ins["events"].append(ev)
-            ins.setdefault("spec", []).append(speculative)
+            ins["ids"].append(self._launch_id)
 
     def commit(self):
         """Make the last speculative solve's outputs and warm-start state the current ones."""
@@ -286,6 +341,7 @@ class PHEngine:
             setattr(self, k, self._spec[k])
             self._spec[k] = cur
         _lib.check(self.lib.phgpu_commit(self.h), "phgpu_commit")
+        self._cur_id = self._spec_id
 
     def _status_counts(self):
         if not hasattr(self, "_counts_dev"):
@@ -303,19 +359,18 @@ class PHEngine:
         return int(c[1:].sum())
 
     def count_not_optimal_async(self):
-        """The same count for the solve just launched, without waiting: its statistics
-        (phgpu_solve_stats, accumulated in the path-6 kernels) go to pinned host memory
-        behind an event; ``pending_not_optimal`` reads them (free after the next host
-        synchronisation)."""
-        if not hasattr(self, "_stats_host"):
-            self._stats_host = torch.zeros(6, dtype=torch.int64).pin_memory()
-            self._stats_ev = torch.cuda.Event()
-        _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(self._stats_host), self._stream()), "phgpu_solve_stats")
-        self._stats_ev.record()
+        """The same count for the current solve, without device work now: the next
+        ``update`` writes its statistics (accumulated in the path-6 kernels) to pinned host
+        memory with the convergence value, so ``pending_not_optimal`` after the next
+        convergence readback costs nothing; without an update in between it asks
+        phgpu_solve_stats (one small copy and a wait)."""
+        self._gripe_id = self._cur_id
 
     def pending_not_optimal(self):
-        self._stats_ev.synchronize()
-        return int(self._stats_host[1:4].sum())
+        st = self._stats_of(self._gripe_id)
+        if st is None:  # a later launch replaced the library's statistics: count statuses
+            return self.count_not_optimal()
+        return int(st[1:4].sum())
 
     def compute_xbar_partials(self):
         _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),
@@ -329,28 +384,56 @@ class PHEngine:
         return self.node_buf
 
     def update(self, update_W=True):
-        """Scatter x̄, W += rho (x - x̄), local conv (phbase.py:90-103, 293-339)."""
-        _lib.check(self.lib.phgpu_ph_update(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
-                                            _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
-                                            _ptr(self.conv_buf), self._stream()), "phgpu_ph_update")
+        """Scatter x̄, W += rho (x - x̄), local conv (phbase.py:90-103, 293-339).  One rank:
+        conv goes straight to pinned host memory (no copy launch; with several ranks it
+        stays on the device for the all-reduce).  The last launch's statistics go to
+        pinned host memory in the same kernel (the gripe and the instrumentation read
+        them there)."""
+        self._conv_zero_copy = self.comm.size == 1
+        conv = self._conv_host if self._conv_zero_copy else self.conv_buf
+        self._upd_seq += 1
+        self._upd_marks = {k: v for k, v in self._upd_marks.items() if k > self._upd_seq - 4}
+        self._upd_marks[self._upd_seq] = None
+        stats = None
+        if self._launch_id:
+            ins = getattr(self, "_ins", None)
+            if ins is not None and ins["next"] < ins["rows"].shape[0]:
+                rows, r = ins["rows"], ins["next"]
+                ins["next"] += 1
+            else:
+                rows, r = self._stats_rows, 0
+                self._row_of = {k: v for k, v in self._row_of.items() if v[0] is not rows}
+            self._row_of[self._launch_id] = (rows, r, self._upd_seq)
+            stats = rows[r]
+        _lib.check(self.lib.phgpu_ph_update_ex(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
+                                               _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
+                                               _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_update_ex")
 
     def convergence_diff(self):
         """phbase.py:330-343: sum over ranks of per-rank means, / n_proc (host float)."""
+        if self._conv_zero_copy:
+            self._marker().synchronize()
+            return float(self._conv_host[0])
         self._allreduce_sum_(self.conv_buf)
         return float(self.conv_buf.item()) / self.comm.size
 
     def convergence_diff_async(self):
-        """Start the same readback without waiting (pinned copy behind an event):
-        ``convergence_wait`` returns it; work queued after this call does not delay it."""
-        if not hasattr(self, "_conv_host"):
-            self._conv_host = torch.zeros(1, dtype=torch.float64).pin_memory()
-            self._conv_ev = torch.cuda.Event()
+        """Start the same readback without waiting (an event behind the update's host
+        write, or the all-reduce and a pinned copy): ``convergence_wait`` returns it; work
+        queued after this call does not delay it."""
+        if self._conv_zero_copy:
+            # the update's marker; while instrumenting, the next solve's start event
+            self._conv_ev = None if self._recording() else self._marker()
+            self._conv_seq = self._upd_seq
+            return
         self._allreduce_sum_(self.conv_buf)
         self._conv_host.copy_(self.conv_buf, non_blocking=True)
+        self._conv_ev = torch.cuda.Event()
         self._conv_ev.record()
 
     def convergence_wait(self):
-        self._conv_ev.synchronize()
+        ev = self._conv_ev if self._conv_ev is not None else self._marker(self._conv_seq)
+        ev.synchronize()
         return float(self._conv_host[0]) / self.comm.size
 
     def expectations(self):
