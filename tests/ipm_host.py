@@ -81,9 +81,11 @@ class _Params(ctypes.Structure):
                    ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP)])
 
 
-def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13):
+def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13,
+          x_in=None, y_in=None):
     """Solve every scenario of a ScenarioBatch with the host-compiled kernel.  W / rho /
-    xbar: [S, nn] (None = that PH term off).  Returns x [S, n], y [S, m], obj, bound,
+    xbar: [S, nn] (None = that PH term off); x_in / y_in [S, n] / [S, m]: the warm state
+    (the previous solve's x and y).  Returns x [S, n], y [S, m], obj, bound,
     status (-1 = left for the PDHG fallback), iters."""
     import mpisppy_amd._lib as L
     src, _ = L.ipm_source(batch)
@@ -121,7 +123,8 @@ def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_i
     keep.append(cnt)
     p.S, p.W_on, p.prox_on = S, int(W is not None), int(rho is not None)
     p.eps_rel, p.eps_abs, p.max_ipm, p.eps_tight = eps_rel, eps_abs, max_ipm, eps_tight
-    p.x_in, p.y_in = None, None
+    p.x_in = ptr(T(x_in)) if x_in is not None else None
+    p.y_in = ptr(T(y_in)) if y_in is not None else None
     st16 = np.zeros(16, dtype=np.uint64)
     keep.append(st16)
     p.stats, p.stats_zero = st16.ctypes.data, st16[8:].ctypes.data

@@ -97,3 +97,29 @@ def test_host_kernel_aircond_lp_vs_highs():
         ax = b.dense_A(s) @ x[s]
         assert np.all(np.abs(ax - b.rl[s]) <= 1e-6 * (1 + np.abs(b.rl[s])))
         assert np.all(x[s] >= b.lb[s] - 1e-9) and np.all(x[s] <= b.ub[s] + 1e-9)
+
+
+def test_host_kernel_warm_start_vs_oracle():
+    """The warm start (a PH iteration's solve from the previous x / y, jit_ipm.hip.in
+    IPM_WARM) reaches the same exact prox-QP solutions as the cold start, in fewer
+    iterations."""
+    from mpisppy_amd.examples import farmer
+    from oracle import farmer_vec as FV
+    S = 1024
+    names = farmer.scenario_names_creator(S)
+    b = _farmer(S)
+    ph = FV.FarmerVecPH(names, 1)
+    ph.iter0()
+    ph.iterk_loop(2)
+    W, xb, rho = ph.W.copy(), ph.xbar.copy(), ph.rho.copy()
+    xp, yp, *_ = ipm_host.solve(b, W=W, rho=rho, xbar=xb, eps_rel=1e-9)    # the previous solve
+    ph.iterk_loop(1)
+    W, xb, rho = ph.W.copy(), ph.xbar.copy(), ph.rho.copy()
+    xo, oo = FV.prox(ph.bp, ph.sl, ph.f0, W, xb, rho, ph.total)
+    _, _, _, _, stc, itc = ipm_host.solve(b, W=W, rho=rho, xbar=xb, eps_rel=1e-9)
+    x, y, obj, bd, st, it = ipm_host.solve(b, W=W, rho=rho, xbar=xb, eps_rel=1e-9, x_in=xp, y_in=yp)
+    assert (st == 0).all() and (stc == 0).all()
+    assert np.abs(x[:, b.nonant_col] - xo).max() <= 1e-5
+    assert (np.abs(obj - oo) / np.abs(oo)).max() <= 1e-9
+    assert np.all(bd <= obj + 1e-9 * np.abs(obj))
+    assert it.mean() < 0.8 * itc.mean() and it.max() < itc.max(), (it.mean(), itc.mean(), it.max(), itc.max())
