@@ -2211,7 +2211,7 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     if (path == 6) {
         const int rc6 = ipm_prepare(h, st);
         if (rc6) return rc6;
-        if (o.kernel == 0 && h->ipm->private_bytes > IPM_SPILL_MAX) {
+        if (o.kernel == 0 && h->ipm->private_bytes > ipm_spill_max()) {
             h->ipm_off = 1;  // the automatic choice falls back to the handle's PDHG path
             path = default_path(h);
         }

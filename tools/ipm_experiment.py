@@ -23,6 +23,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--S", type=int, default=2048)
+    ap.add_argument("--model", choices=["farmer", "aircond"], default="farmer")
+    ap.add_argument("--bf", default="8,8,16")
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--tmpl", default=os.path.join(ROOT, "mpi-sppy-1_amd", "csrc", "jit_ipm.hip.in"))
     ap.add_argument("--eps-tight", type=float, default=1e-13)
@@ -36,7 +38,15 @@ def main():
     import ipm_host
     import mpisppy_amd._lib as L
     from mpisppy_amd.examples import farmer
-    b = farmer.batch_creator(farmer.scenario_names_creator(a.S), crops_multiplier=1, num_scens=a.S)
+    if a.model == "farmer":
+        b = farmer.batch_creator(farmer.scenario_names_creator(a.S), crops_multiplier=1, num_scens=a.S)
+    else:
+        from mpisppy_amd.examples import aircond
+        from bench import AIRCOND_KW
+        bf = [int(v) for v in a.bf.split(",")]
+        b = aircond.batch_creator(aircond.scenario_names_creator(int(np.prod(bf))), branching_factors=bf,
+                                  **AIRCOND_KW)
+        a.S = b.S
     src, _ = L.ipm_source(b)
     tmpl = open(a.tmpl).read()
     src = src[:src.index("// jit_ipm.hip.in --")] + tmpl
@@ -59,9 +69,13 @@ def main():
         xs = [x]
         W = np.zeros((a.S, nn))
         for k in range(a.iters):
-            xb = (prob[:, None] * x[:, nc]).sum(0) / prob.sum()
-            W = W + rho * (x[:, nc] - xb)
-            xbar = np.broadcast_to(xb, (a.S, nn)).copy()
+            xbar = np.zeros((a.S, nn))
+            for kk in range(nn):  # x̄ per tree node of the nonant's depth (phbase.py:54-79)
+                g = b.node_of[:, b.nonant_depth[kk]]
+                num = np.bincount(g, prob * x[:, nc[kk]])
+                den = np.bincount(g, prob)
+                xbar[:, kk] = (num / np.where(den > 0, den, 1))[g]
+            W = W + rho * (x[:, nc] - xbar)
             x, y, obj, bound, st, it = ipm_host.solve(b, W=W, rho=rho, xbar=xbar, eps_rel=a.eps,
                                                       eps_tight=a.eps_tight,
                                                       x_in=x if a.warm else None, y_in=y if a.warm else None)
