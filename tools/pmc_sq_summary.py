@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc SQ passes of the solve kernel (issue-side roofline).
 
-usage: python tools/pmc_sq_summary.py out.json passA.csv [passB.csv ...]
+usage: python tools/pmc_sq_summary.py [--kernel=NAME] out.json passA.csv [passB.csv ...]
+(--kernel: only dispatches whose kernel name starts with NAME; default: every "k_solve")
 
 For every counter the mean over the solve dispatches after the first (the first is the
 cold Iter0 LP) is reported, then derived figures:
@@ -21,12 +22,17 @@ import sys
 SIMDS = 256 * 4
 FP64_PEAK_TF = 78.6
 
-out_json, paths = sys.argv[1], sys.argv[2:]
+args = sys.argv[1:]
+want = "k_solve"
+if args and args[0].startswith("--kernel="):
+    want = args.pop(0).split("=", 1)[1]
+out_json, paths = args[0], args[1:]
 vals = collections.defaultdict(list)
 durs = []
 name = None
 for p in paths:
-    rows = [r for r in csv.DictReader(open(p)) if "k_solve" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(p)) if r["Kernel_Name"].startswith(want)
+            if want != "k_solve" or "k_solve" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     per = collections.defaultdict(dict)
     for r in rows:
