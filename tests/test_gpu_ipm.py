@@ -279,3 +279,60 @@ def test_lane_groups_random_batches(gpu, ipm_lanes, S, with_q):
 @pytest.mark.parametrize("kind,code", [("primal", 2), ("dual", 3)])
 def test_lane_groups_hand_infeasible_scenarios_to_the_pdhg(gpu, ipm_lanes, kind, code):
     test_path6_hands_infeasible_scenarios_to_the_pdhg(gpu, kind, code)
+
+
+@pytest.mark.parametrize("model,S,lanes", [("farmer", 8192, 8), ("farmer", 16384, 4), ("farmer", 32768, 1),
+                                           ("aircond", 16384, 4)])
+def test_lane_policy_by_share(gpu, model, S, lanes):
+    """ipm_lanes (solve_ipm.inc): lane groups of 8 for <= 8,192 local scenarios, of 4 for
+    <= 16,384 and for a pattern whose one-lane module spills (aircond), one lane above --
+    and the automatic solve stays on path 6 without scratch."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import aircond, farmer
+    if model == "farmer":
+        b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=1, num_scens=S)
+    else:
+        kw = {"Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50, "mu_dev": 0, "sigma_dev": 40,
+              "start_seed": 0}
+        b = aircond.batch_creator(aircond.scenario_names_creator(S), branching_factors=[8, 32, 64], **kw)
+    e = PHEngine(b, device="cuda:0")
+    e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
+    ii = e.ipm_info()
+    assert e.kernel_info()["path"] == 6 and ii["lanes"] == lanes and ii["scratch_bytes"] == 0, ii
+    assert (e.host("status") == 0).all()
+    e.close()
+
+
+def test_warm_start_cuts_iterations_same_answers(gpu):
+    """The warm start (jit_ipm.hip.in IPM_WARM): a PH solve from the previous x / y needs
+    fewer IPM iterations than from the cold start and reaches the same solutions (1e-5
+    absolute on x, 1e-9 relative on the objectives, both against the exact oracle)."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import farmer
+    from oracle import farmer_vec as FV
+    S = 4096
+    names = farmer.scenario_names_creator(S)
+    ph = FV.FarmerVecPH(names, 1)
+    ph.iter0()
+    ph.iterk_loop(2)
+    b = farmer.batch_creator(names, crops_multiplier=1, num_scens=S)
+    runs = {}
+    for warm in (False, True):
+        e = PHEngine(b, device="cuda:0")
+        e.set_rho(ph.rho)
+        e.solve(_lib.default_options(eps_rel=1e-9), warm=False)      # the state a PH solve starts from
+        e.set_W(ph.W)
+        e.set_xbar(ph.xbar)
+        e.set_terms(1, 1)
+        e.solve(_lib.default_options(eps_rel=1e-9), warm=warm)
+        runs[warm] = (e.host("x")[:, b.nonant_col].copy(), e.host("obj").copy(), e.host("iters").copy(),
+                      e.host("status").copy())
+        e.close()
+    xo, oo = FV.prox(ph.bp, ph.sl, ph.f0, ph.W, ph.xbar, ph.rho, ph.total)
+    for warm, (x, obj, it, st) in runs.items():
+        assert (st == 0).all()
+        assert np.abs(x - xo).max() <= 1e-5, (warm, np.abs(x - xo).max())
+        assert (np.abs(obj - oo) / np.abs(oo)).max() <= 1e-9
+    assert runs[True][2].mean() < 0.8 * runs[False][2].mean(), (runs[True][2].mean(), runs[False][2].mean())
