@@ -271,8 +271,7 @@ def roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir):
             "launch_ms": launch_ms, "scenario_iters_per_launch": units, "flops_per_scenario_iter": F,
             "ipm": {k: ipm[k] for k in ("rows", "factor_entries", "scratch_bytes", "compile_s")},
             "note": ("achieved = F x IPM scenario-iterations per launch / mean HIP-event launch time (the "
-                     "library's events ride on the IPM dispatch and on the dispatch of the PDHG fallback "
-                     "kernel over the IPM's fallback list, phgpu_timing_begin; no marker packets); F = "
+                     "launch includes the PDHG fallback kernel over the IPM's fallback list); F = "
                      "ipm_flops_per_iter (bench.py)")}
 
 

@@ -204,17 +204,6 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
                     double* W, const double* rho, int update_W, double* conv_local,
                     void* stream);
 
-/* Time the next max_solves solves (phgpu_solve / phgpu_solve_deferred) with HIP events the
- * library owns: on path 6 the start / stop events ride on the solve's first and last kernel
- * dispatch (hipExtModuleLaunchKernel, no marker packets in the stream); on the other paths
- * they are recorded on the stream around the solve.  phgpu_timing_begin(h, 0) stops timing.
- * (The bench's per-launch roofline; a marker packet idles the GPU ~5.6 us per record.) */
-int phgpu_timing_begin(phgpu_handle h, int32_t max_solves);
-
-/* Milliseconds of the timed solves so far, in launch order, into ms[0..*n) (at most cap);
- * waits for the last one and ends the timing (the events are released). */
-int phgpu_timing_end(phgpu_handle h, float* ms, int32_t cap, int32_t* n);
-
 /* phgpu_ph_update, plus: stats_out (int64[6], may be NULL) receives the statistics of
  * the handle's last solve launch as phgpu_solve_stats reports them, written by the same
  * kernel that writes conv_local.  conv_local and stats_out may be host-mapped pinned

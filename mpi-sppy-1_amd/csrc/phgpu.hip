@@ -15,7 +15,6 @@
 //   _Compute_Xbar / Update_W / conv     phbase.py:27-107, 293-343
 //   Ebound / Eobjective / E1 / feas     spopt.py:310-439
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdarg.h>
@@ -92,10 +91,6 @@ struct phgpu_state {
     int pk_A, pk_C, pk_Q, pk_DC, pk_LB, pk_UB, pk_RL, pk_RU, pk_DR, pk_RLH, pk_RUH, pk_X, pk_Y, pk_W, pk_RHO,
         pk_XB;
     int last_path;       // path of the last solve (whose layout holds the warm start)
-    // phgpu_timing_begin: event pairs for the next tm_n solves (tm_next used so far); the
-    // current solve's pair, consumed by path 6's first / last dispatch (tm_start / tm_stop)
-    hipEvent_t *tm_ev, tm_start, tm_stop;
-    int tm_n, tm_next;
     int scen_set;
     // 1 if some wave of local scenarios spans two nodes at a nonant's depth (its x̄
     // contributions go to node_buf by atomics, so node_buf is cleared by a memset first);
@@ -2117,37 +2112,8 @@ static int default_path(const phgpu_state* h) {
     return h->default_kernel;
 }
 
-static int solve_dispatch(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
-                          double* obj, double* bound, int32_t* status, int32_t* iters, void* stream);
-
-// a solve, timed by the next event pair of phgpu_timing_begin if any: on path 6 the events
-// ride on the solve's first and last kernel dispatch (hipExtModuleLaunchKernel: no marker
-// packets); on the other paths they are recorded on the stream around it
 static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
                       double* obj, double* bound, int32_t* status, int32_t* iters, void* stream) {
-    if (!h) return set_err(-1, "null handle");
-    if (h->tm_next >= h->tm_n)
-        return solve_dispatch(h, opt, warm_start, defer, x, y, obj, bound, status, iters, stream);
-    hipStream_t st = (hipStream_t)stream;
-    hipEvent_t t0 = h->tm_ev[2 * h->tm_next], t1 = h->tm_ev[2 * h->tm_next + 1];
-    ++h->tm_next;
-    const int k = opt ? opt->kernel : 0;
-    const bool on6 = k == 6 || (k == 0 && !h->shared && default_path(h) == 6);
-    if (!on6) HIPCHK(hipEventRecord(t0, st));
-    h->tm_start = on6 ? t0 : nullptr;
-    h->tm_stop = on6 ? t1 : nullptr;
-    const int rc = solve_dispatch(h, opt, warm_start, defer, x, y, obj, bound, status, iters, stream);
-    if (!on6) HIPCHK(hipEventRecord(t1, st));
-    else if (h->tm_start || h->tm_stop) {  // predicted path 6, but it took another path
-        HIPCHK(hipEventRecord(t0, st));
-        HIPCHK(hipEventRecord(t1, st));
-    }
-    h->tm_start = h->tm_stop = nullptr;
-    return rc;
-}
-
-static int solve_dispatch(phgpu_handle h, const phgpu_options* opt, int warm_start, int defer, double* x, double* y,
-                          double* obj, double* bound, int32_t* status, int32_t* iters, void* stream) {
     if (!h) return set_err(-1, "null handle");
     if (!x || !obj || !bound || !status) return set_err(-1, "null output pointer");
     if (defer && h->shared)
@@ -2474,48 +2440,6 @@ __global__ void __launch_bounds__(SC_T) k_solve_stats(const int32_t* __restrict_
     if (threadIdx.x < 6) out[threadIdx.x] = c[threadIdx.x];
 }
 
-static void timing_free(phgpu_state* h) {
-    for (int i = 0; i < 2 * h->tm_n; ++i) (void)hipEventDestroy(h->tm_ev[i]);
-    free(h->tm_ev);
-    h->tm_ev = nullptr;
-    h->tm_n = h->tm_next = 0;
-}
-
-extern "C" int phgpu_timing_begin(phgpu_handle h, int32_t max_solves) {
-    if (!h || max_solves < 0) return set_err(-1, "bad argument");
-    timing_free(h);
-    if (max_solves == 0) return 0;
-    h->tm_ev = (hipEvent_t*)calloc((size_t)2 * max_solves, sizeof(hipEvent_t));
-    if (!h->tm_ev) return set_err(-3, "out of host memory");
-    for (int i = 0; i < 2 * max_solves; ++i) {
-        if (hipEventCreate(&h->tm_ev[i]) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipEventDestroy(h->tm_ev[j]);
-            free(h->tm_ev);
-            h->tm_ev = nullptr;
-            return set_err(-2, "hipEventCreate failed");
-        }
-    }
-    h->tm_n = max_solves;
-    h->tm_next = 0;
-    return 0;
-}
-
-extern "C" int phgpu_timing_end(phgpu_handle h, float* ms, int32_t cap, int32_t* n) {
-    if (!h || !n || (cap > 0 && !ms)) return set_err(-1, "null argument");
-    const int k = std::min(h->tm_next, std::max(cap, 0));
-    int rc = 0;
-    for (int i = 0; i < k; ++i) {
-        float t = NAN;
-        if (hipEventSynchronize(h->tm_ev[2 * i + 1]) != hipSuccess ||
-            hipEventElapsedTime(&t, h->tm_ev[2 * i], h->tm_ev[2 * i + 1]) != hipSuccess)
-            rc = set_err(-2, "timing event %d: %s", i, hipGetErrorString(hipGetLastError()));
-        ms[i] = t;
-    }
-    *n = k;
-    timing_free(h);
-    return rc;
-}
-
 extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
     if (!h || !out) return set_err(-1, "null argument");
     if (!h->last_status) return set_err(-1, "phgpu_solve_stats: no solve yet");
@@ -2648,7 +2572,6 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
         if (h->ipm->mod) (void)hipModuleUnload(h->ipm->mod);
         delete h->ipm;
     }
-    if (h->tm_ev) timing_free(h);
     if (h->ipm_list) (void)hipFree(h->ipm_list);
     if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
     if (h->ipm_stats) (void)hipFree(h->ipm_stats);

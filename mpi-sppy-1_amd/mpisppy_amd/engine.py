@@ -213,53 +213,42 @@ class PHEngine:
         self._bind()
 
     # -------------------------------------------------------------- instrumentation
-    # all-reduces timed with stream events while instrumenting (each event record is a
-    # marker packet; the rest are counted and the mean extrapolated)
     _AR_TIMED = 8
 
     def instrument(self, max_solves):
-        """Record the next ``max_solves`` phgpu_solve launches: their duration by HIP events
-        the library attaches to the launch's first and last kernel dispatch
-        (phgpu_timing_begin; no marker packets on path 6) and their statistics (status
-        counts, iteration sum and maximum, written by the next update kernel).  Used by
-        bench.py for the per-launch roofline inside its timed region."""
+        """Record the next ``max_solves`` phgpu_solve launches: HIP events on the launch
+        stream around each launch and the launch's statistics (phgpu_solve_stats: status
+        counts, iteration sum and maximum; one 48-byte copy after the launch, outside the
+        event pair).  Used by bench.py for the per-launch roofline inside its timed region."""
         self._ins = {"events": [], "ids": [], "max": int(max_solves), "ar_events": [], "ar_count": 0,
-                     "rows": torch.zeros((max_solves + 4, 6), dtype=torch.int64).pin_memory(), "next": 0,
-                     "ms": None}
-        _lib.check(self.lib.phgpu_timing_begin(self.h, int(max_solves)), "phgpu_timing_begin")
+                     "rows": torch.zeros((max_solves + 4, 6), dtype=torch.int64).pin_memory(), "next": 0}
 
     def instrumented(self):
         """[(launch ms, scenario-iterations)] of the recorded launches (syncs)."""
-        return [(ms, int(st[4])) for ms, st in self._ins_stats()]
+        return [(a.elapsed_time(b), int(st[4])) for (a, b), st in self._ins_stats()]
 
     def instrumented_not_optimal(self):
         """Scenarios not OPTIMAL in each recorded launch."""
         return [int(st[1:4].sum()) for _, st in self._ins_stats()]
 
     def _ins_stats(self):
-        """[(launch ms, stats[6])] of the recorded launches whose statistics are known: the
+        """[(event pair, stats[6])] of the recorded launches whose statistics are known: the
         update after a launch wrote them (phgpu_ph_update_ex), or the launch is the last
         one (phgpu_solve_stats).  Synchronises."""
         ins = getattr(self, "_ins", None)
         if not ins:
             return []
         torch.cuda.synchronize(self.device)
-        if ins["ms"] is None:
-            cap = max(1, ins["max"])
-            ms = (ctypes.c_float * cap)()
-            n = ctypes.c_int32(0)
-            _lib.check(self.lib.phgpu_timing_end(self.h, ms, cap, ctypes.byref(n)), "phgpu_timing_end")
-            ins["ms"] = [float(ms[i]) for i in range(n.value)]
         out = []
-        for k, lid in enumerate(ins["ids"]):
+        for ev, lid in zip(ins["events"], ins["ids"]):
             st = self._stats_of(lid)
-            if st is not None and k < len(ins["ms"]):
-                out.append((ins["ms"][k], st))
+            if st is not None:
+                out.append((ev, st))
         return out
 
     def _recording(self):
         ins = getattr(self, "_ins", None)
-        return ins is not None and len(ins["ids"]) < ins["max"]
+        return ins is not None and len(ins["events"]) < ins["max"]
 
     def _marker(self, seq=None):
         """The event behind update ``seq`` (default: the last one), recorded now if it has
@@ -300,8 +289,10 @@ class PHEngine:
     def _allreduce_sum_(self, t):
         """comm.allreduce_sum_ with HIP events around it while instrumenting."""
         ins = getattr(self, "_ins", None)
-        if ins is None or self.comm.size == 1 or len(ins["ids"]) >= ins["max"]:
+        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["max"]:
             return self.comm.allreduce_sum_(t)
+        # the first _AR_TIMED all-reduces are timed (each event record is a marker packet
+        # that idles the GPU ~5.6 us); the rest are counted and the mean extrapolated
         ins["ar_count"] += 1
         if len(ins["ar_events"]) >= self._AR_TIMED:
             return self.comm.allreduce_sum_(t)
@@ -331,6 +322,11 @@ class PHEngine:
             out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
         rec = self._recording()
+        if rec:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            if self._upd_seq and self._upd_marks.get(self._upd_seq) is None:
+                self._upd_marks[self._upd_seq] = ev[0]   # the update's marker, shared
         self._launch_id += 1
         if speculative:
             self._spec_id = self._launch_id
@@ -342,8 +338,10 @@ class PHEngine:
                       _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
                    "phgpu_solve_deferred" if speculative else "phgpu_solve")
         if rec:
-            # timed by the library's events (phgpu_timing_begin); the statistics come with the
-            # next update (phgpu_ph_update_ex), the last launch's from phgpu_solve_stats
+            ev[1].record()
+            # the launch's statistics come with the next update (phgpu_ph_update_ex), the
+            # last launch's from phgpu_solve_stats after the loop: no copy per launch
+            ins["events"].append(ev)
             ins["ids"].append(self._launch_id)
 
     def commit(self):
@@ -434,7 +432,8 @@ class PHEngine:
         write, or the all-reduce and a pinned copy): ``convergence_wait`` returns it; work
         queued after this call does not delay it."""
         if self._conv_zero_copy:
-            self._conv_ev = self._marker()   # the update's marker
+            # the update's marker; while instrumenting, the next solve's start event
+            self._conv_ev = None if self._recording() else self._marker()
             self._conv_seq = self._upd_seq
             return
         self._allreduce_sum_(self.conv_buf)

@@ -118,21 +118,3 @@ def test_update_ex_rejects_stats_before_solve(gpu):
     assert rc != 0
     e.close()
 
-
-def test_timing_events_on_dispatches(gpu):
-    """phgpu_timing_begin / _end: the library's events ride on path 6's first and last
-    dispatch and are stream-recorded around the other paths' solves; every timed solve gets
-    a positive duration, in launch order, and timing stops after max_solves."""
-    from mpisppy_amd import _lib
-    e = _engine("farmer", 3000)
-    e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
-    _lib.check(e.lib.phgpu_timing_begin(e.h, 3), "phgpu_timing_begin")
-    for k in (0, 2, 6, 0):                      # the fourth is past max_solves: untimed
-        e.solve(_lib.default_options(eps_rel=1e-9, kernel=k), warm=True)
-    ms = (ctypes.c_float * 8)()
-    n = ctypes.c_int32(0)
-    _lib.check(e.lib.phgpu_timing_end(e.h, ms, 8, ctypes.byref(n)), "phgpu_timing_end")
-    assert n.value == 3
-    assert all(0.0 < ms[i] < 1000.0 for i in range(3)), list(ms)[:3]
-    assert (e.host("status") == 0).all()
-    e.close()
