@@ -336,3 +336,43 @@ def test_warm_start_cuts_iterations_same_answers(gpu):
         assert np.abs(x - xo).max() <= 1e-5, (warm, np.abs(x - xo).max())
         assert (np.abs(obj - oo) / np.abs(oo)).max() <= 1e-9
     assert runs[True][2].mean() < 0.8 * runs[False][2].mean(), (runs[True][2].mean(), runs[False][2].mean())
+
+
+@pytest.mark.parametrize("ipm_lanes", [1, 4], indirect=True)
+@pytest.mark.parametrize("S,with_q", [(67, False), (130, True)])
+def test_warm_started_ph_terms_on_random_batches(gpu, ipm_lanes, S, with_q):
+    """A PH-like warm-started solve (W and the prox term on the nonant columns, the start
+    from the previous solve's x / y) on random batches with ranged, equality, one-sided and
+    free rows and infinite bounds, one lane and lane groups: the same optima as the oracle's
+    QP IPM on the W- and prox-augmented problems."""
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd import _lib
+    from oracle.lpqp import solve_qp_ipm
+    b = _random_lp_batch(S, 9, 6, 0.5, seed=S + 11, with_q=with_q)
+    e = PHEngine(b, device="cuda:0")
+    e.solve(_lib.default_options(kernel=6), warm=False)                 # Iter0
+    rng = np.random.default_rng(S)
+    nc = np.asarray(b.nonant_col)
+    x0 = e.host("x")[:, nc]
+    xbar = np.broadcast_to(x0.mean(0), x0.shape).copy()
+    W = rng.normal(scale=0.3, size=x0.shape)
+    rho = np.full(x0.shape, 0.7)
+    e.set_rho(rho)
+    e.set_W(W)
+    e.set_xbar(xbar)
+    e.set_terms(1, 1)
+    e.solve(_lib.default_options(kernel=6), warm=True)                  # warm: from Iter0's x / y
+    st, obj, x = e.host("status"), e.host("obj"), e.host("x")
+    assert (st == _lib.OPTIMAL).all(), st
+    assert e.ipm_info()["lanes"] == ipm_lanes
+    for s in range(S):
+        c = b.c[s].copy()
+        q = b.q[s].copy()
+        c[nc] += W[s] - rho[s] * xbar[s]
+        q[nc] += rho[s]
+        xr, ob, rc = solve_qp_ipm(b.dense_A(s), b.rl[s], b.ru[s], b.lb[s], b.ub[s], c, q)
+        assert rc == 0
+        ob += 0.5 * float(np.sum(rho[s] * xbar[s] ** 2))                 # the prox constant
+        assert abs(obj[s] - ob) <= OBJ_REL * max(1.0, abs(ob)), (s, obj[s], ob)
+        assert np.abs(x[s][nc] - xr[nc]).max() <= 1e-5 * (1 + np.abs(xr[nc]).max()), (s, x[s][nc], xr[nc])
+    e.close()
