@@ -217,9 +217,11 @@ class PHEngine:
 
     def instrument(self, max_solves):
         """Record the next ``max_solves`` phgpu_solve launches: HIP events on the launch
-        stream around each launch and the launch's statistics (phgpu_solve_stats: status
-        counts, iteration sum and maximum; one 48-byte copy after the launch, outside the
-        event pair).  Used by bench.py for the per-launch roofline inside its timed region."""
+        stream around each launch (the start event doubles as the update's marker the host
+        waits on for conv) and the launch's statistics (status counts, iteration sum and
+        maximum; written to pinned memory by the next update kernel, the last launch's by
+        phgpu_solve_stats).  Used by bench.py for the per-launch roofline inside its timed
+        region."""
         self._ins = {"events": [], "ids": [], "max": int(max_solves), "ar_events": [], "ar_count": 0,
                      "rows": torch.zeros((max_solves + 4, 6), dtype=torch.int64).pin_memory(), "next": 0}
 
