@@ -214,6 +214,14 @@ int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double* node_buf, 
                        double* W, const double* rho, int update_W, double* conv_local,
                        int64_t* stats_out, void* stream);
 
+/* phgpu_ph_reduce + phgpu_ph_update_ex for a single rank (no cross-rank sum of node_buf
+ * between them), in fewer launches when every nonant's local scenarios share one node (a
+ * two-stage problem) and nn <= 16: the x̄ final sum is folded into the update kernel.
+ * Same outputs: node_buf (the local sums), xbar, W, conv_local, stats_out. */
+int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node_buf, double* xbar, double* W,
+                        const double* rho, int update_W, double* conv_local, int64_t* stats_out,
+                        void* stream);
+
 /* Local probability-weighted sums (spopt.py:310-439) into out[5]:
  *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
  *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s feasible} prob_s, where feasible

@@ -96,6 +96,9 @@ struct phgpu_state {
     // contributions go to node_buf by atomics, so node_buf is cleared by a memset first);
     // 0 if none does (k_xbar_partial clears node_buf itself); -1 not yet known
     int xbar_mixed;
+    // 1 if every nonant's local scenarios share one node (two-stage problems): a single
+    // rank's x̄ final sum can then be folded into the update kernel (phgpu_ph_step_local)
+    int xbar_single;
     int* qhead;  // work-queue head of the persistent solve kernel
     int num_cus;
     int occ_cache[8];  // workgroups per CU of each solve kernel (0 = not queried yet)
@@ -909,18 +912,21 @@ k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict_
 
 // out[0] |= 1 if some wave of local scenarios spans two nodes at a nonant's depth (the
 // test k_xbar_partial makes per wave)
+// out[1] |= 1 if some local scenario's node at a nonant's depth differs from scenario 0's
 __global__ void __launch_bounds__(BLOCK) k_xbar_mixed(phgpu_state st, int32_t* __restrict__ out) {
     const int64_t S = st.S;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool act = s < S;
-    bool mixed = false;
+    bool mixed = false, multi = false;
     for (int k = 0; k < st.nn; ++k) {
         const int d = st.nonant_depth[k];
         const int gnode = act ? st.node_of[IX(d)] : -1;
         const int g0 = __shfl(gnode, 0, WAVE);
         mixed |= __any(act && gnode != g0) != 0;
+        multi |= __any(act && gnode != st.node_of[(int64_t)d * S]) != 0;
     }
     if (mixed && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(out, 1);
+    if (multi && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(out + 1, 1);
 }
 
 // Ordered segmented sum of the per-wave partials, one block per nonant.  The local
@@ -1058,6 +1064,78 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
     }
     acc = wave_sum(acc);
     if ((threadIdx.x & (WAVE - 1)) == 0) st.part[s / WAVE] = acc;
+}
+
+// phgpu_ph_step_local (one rank, every nonant's scenarios on one node, nn <= XL_NN_MAX):
+// k_xbar_final and k_ph_update in one launch.  Every block sums the per-wave x̄ partials
+// itself, in one fixed order (so every block gets the same bits), block 0 stores them in
+// node_buf; then the scatter / W update / conv partial of k_ph_update, the conv partials
+// going to their own region (cpart) because other blocks are still reading part.
+#define XL_NN_MAX 16
+#define XL_T 1024  // threads per block: every block re-sums the wave partials, so few, large blocks
+__global__ void __launch_bounds__(XL_T)
+k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf,
+                  double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
+                  int update_W, double* __restrict__ cpart) {
+    __shared__ double sa[XL_T / WAVE][XL_NN_MAX], sb[XL_T / WAVE][XL_NN_MAX];
+    __shared__ double xbs[XL_NN_MAX];
+    const int64_t S = st.S;
+    const int nn = st.nn;
+    const int half = st.num_nodes * st.nlen_max;
+    // every nonant at once: strided loads of the contiguous per-wave partials, wave sums,
+    // then the block's waves in order (one barrier)
+    double a[XL_NN_MAX], b[XL_NN_MAX];
+#pragma unroll
+    for (int k = 0; k < XL_NN_MAX; ++k) a[k] = b[k] = 0.0;
+    for (int64_t w = threadIdx.x; w < st.nwaves; w += XL_T) {
+        const double* pw = st.part + w * nn * 2;
+#pragma unroll
+        for (int k = 0; k < XL_NN_MAX; ++k)
+            if (k < nn) {
+                a[k] += pw[2 * k];
+                b[k] += pw[2 * k + 1];
+            }
+    }
+    const int wv = threadIdx.x / WAVE;
+#pragma unroll
+    for (int k = 0; k < XL_NN_MAX; ++k)
+        if (k < nn) {
+            const double ta = wave_sum(a[k]), tb = wave_sum(b[k]);
+            if ((threadIdx.x & (WAVE - 1)) == 0) {
+                sa[wv][k] = ta;
+                sb[wv][k] = tb;
+            }
+        }
+    __syncthreads();
+    if (threadIdx.x < nn) {
+        const int k = threadIdx.x;
+        double ta = 0.0, tb = 0.0;
+#pragma unroll
+        for (int u = 0; u < XL_T / WAVE; ++u) {
+            ta += sa[u][k];
+            tb += sb[u][k];
+        }
+        xbs[k] = ta;
+        if (blockIdx.x == 0) {
+            const int g0 = st.node_of[(int64_t)st.nonant_depth[k] * S];
+            node_buf[g0 * st.nlen_max + st.nonant_off[k]] = ta;
+            node_buf[half + g0 * st.nlen_max + st.nonant_off[k]] = tb;
+        }
+    }
+    __syncthreads();
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0.0;
+    if (s < S) {
+        for (int k = 0; k < nn; ++k) {
+            const double xb = xbs[k];
+            const double xv = x[IX(st.nonant_col[k])];
+            xbar[IX(k)] = xb;
+            if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
+            acc += fabs(xv - xb);
+        }
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & (WAVE - 1)) == 0) cpart[s / WAVE] = acc;
 }
 
 // spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible, prob*optimal.
@@ -1728,8 +1806,9 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         h->num_cus = ncu;
     }
     {
+        // per-wave partials [nwaves * K] + the conv partials of phgpu_ph_step_local [nwaves]
         size_t K = (size_t)(2 * nn > 5 ? 2 * nn : 5);
-        ALLOC(h->part, (size_t)h->nwaves * K);
+        ALLOC(h->part, (size_t)h->nwaves * (K + 1));
         ALLOC(h->part_node, (size_t)h->nwaves * (nn > 0 ? nn : 1));
     }
     (void)rc;
@@ -2455,27 +2534,36 @@ extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
     return 0;
 }
 
+// the x̄ partial sums of phgpu_ph_reduce (node_buf cleared, per-wave partials in part)
+static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipStream_t st) {
+    const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
+    if (h->xbar_mixed < 0) {  // once per scenario data: does any wave span two nodes?
+        int32_t* d = nullptr;
+        int32_t v[2] = {0, 0};
+        HIPCHK(hipMalloc((void**)&d, 2 * sizeof(int32_t)));
+        HIPCHK(hipMemsetAsync(d, 0, 2 * sizeof(int32_t), st));
+        hipLaunchKernelGGL(k_xbar_mixed, grid_for(h->S), dim3(BLOCK), 0, st, *h, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(v, d, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipFree(d));
+        h->xbar_mixed = v[0] ? 1 : 0;
+        h->xbar_single = v[1] ? 0 : 1;
+    }
+    if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
+    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
     if (!h || !x || !node_buf) return set_err(-1, "null argument");
     hipStream_t st = (hipStream_t)stream;
     const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
     if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
                                ? 0 : set_err(-2, "hipMemsetAsync failed");
-    if (h->xbar_mixed < 0) {  // once per scenario data: does any wave span two nodes?
-        int32_t* d = nullptr;
-        int32_t v = 0;
-        HIPCHK(hipMalloc((void**)&d, sizeof(int32_t)));
-        HIPCHK(hipMemsetAsync(d, 0, sizeof(int32_t), st));
-        hipLaunchKernelGGL(k_xbar_mixed, grid_for(h->S), dim3(BLOCK), 0, st, *h, d);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(&v, d, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        HIPCHK(hipFree(d));
-        h->xbar_mixed = v ? 1 : 0;
-    }
-    if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
-    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
-    HIPCHK(hipGetLastError());
+    const int rc = xbar_partials(h, x, node_buf, st);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf);
     HIPCHK(hipGetLastError());
     return 0;
@@ -2509,6 +2597,40 @@ extern "C" int phgpu_ph_update(phgpu_handle h, const double* x, const double* no
                                double* xbar, double* W, const double* rho, int update_W,
                                double* conv_local, void* stream) {
     return phgpu_ph_update_ex(h, x, node_buf, xbar, W, rho, update_W, conv_local, nullptr, stream);
+}
+
+extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node_buf, double* xbar, double* W,
+                                   const double* rho, int update_W, double* conv_local, int64_t* stats_out,
+                                   void* stream) {
+    if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
+        return set_err(-1, "null argument");
+    if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_step_local: stats_out before any solve");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->nn == 0 || h->nn > XL_NN_MAX || h->xbar_mixed != 0 || !h->xbar_single) {
+        // the general route (also the first call, which finds out xbar_mixed / _single)
+        const int rc = phgpu_ph_reduce(h, x, node_buf, stream);
+        if (rc) return rc;
+        return phgpu_ph_update_ex(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, stream);
+    }
+    const int rc = xbar_partials(h, x, node_buf, st);
+    if (rc) return rc;
+    const unsigned long long* src = stats_out ? h->last_stats : nullptr;
+    if (stats_out && !src) {
+        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
+                           h->stats_gen);
+        HIPCHK(hipGetLastError());
+        src = h->stats_gen;
+    }
+    const size_t K = (size_t)(2 * h->nn > 5 ? 2 * h->nn : 5);
+    double* cpart = h->part + (size_t)h->nwaves * K;
+    hipLaunchKernelGGL(k_ph_update_local, dim3((unsigned)((h->S + XL_T - 1) / XL_T)), dim3(XL_T), 0, st, *h, x,
+                       node_buf, xbar, W, rho, update_W ? 1 : 0, cpart);
+    HIPCHK(hipGetLastError());
+    const double scale = 1.0 / ((double)h->S * (double)h->nn);
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)cpart, h->nwaves, 1, scale,
+                       conv_local, src, stats_out);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,

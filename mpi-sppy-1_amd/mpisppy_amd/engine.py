@@ -127,6 +127,7 @@ class PHEngine:
         # statistics straight into pinned host memory, no copy launches): launch ids of the
         # last solve launch, of the solve whose outputs are current and of a pending
         # speculative one; row_of maps a launch id to the stats row an update wrote for it.
+        self._xbar_pending = False   # compute_xbar(lazy=True) left x̄ to the next update
         self._launch_id = self._cur_id = self._spec_id = 0
         self._gripe_id = 0
         self._row_of = {}
@@ -315,6 +316,7 @@ class PHEngine:
         test stops the loop).  An uncommitted speculative solve changes nothing: its
         outputs stay in the spare set and the library keeps its warm-start state in a
         second slot that only phgpu_commit makes current (include/phgpu.h)."""
+        self._flush_xbar()
         o = options if options is not None else _lib.default_options()
         if speculative:
             if not hasattr(self, "_spec"):
@@ -389,11 +391,22 @@ class PHEngine:
                    "phgpu_ph_reduce")
         return self.node_buf
 
-    def compute_xbar(self):
-        """Local partials + cross-rank sum (phbase.py:27-87); result left in node_buf."""
+    def compute_xbar(self, lazy=False):
+        """Local partials + cross-rank sum (phbase.py:27-87); result left in node_buf.
+        ``lazy`` (PHBase.Compute_Xbar with one rank): nothing is launched yet -- the next
+        ``update`` does x̄ and the update together (phgpu_ph_step_local: one launch fewer
+        for two-stage problems); anything that reads node_buf first computes it."""
+        if lazy and self.comm.size == 1:
+            self._xbar_pending = True
+            return None
+        self._xbar_pending = False
         self.compute_xbar_partials()
         self._allreduce_sum_(self.node_buf)
         return self.node_buf
+
+    def _flush_xbar(self):
+        if getattr(self, "_xbar_pending", False):
+            self.compute_xbar()
 
     def update(self, update_W=True):
         """Scatter x̄, W += rho (x - x̄), local conv (phbase.py:90-103, 293-339).  One rank:
@@ -417,6 +430,12 @@ class PHEngine:
                 self._row_of = {k: v for k, v in self._row_of.items() if v[0] is not rows}
             self._row_of[self._launch_id] = (rows, r, self._upd_seq)
             stats = rows[r]
+        if getattr(self, "_xbar_pending", False):
+            self._xbar_pending = False
+            _lib.check(self.lib.phgpu_ph_step_local(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
+                                                    _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
+                                                    _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_step_local")
+            return
         _lib.check(self.lib.phgpu_ph_update_ex(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
                                                _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
                                                _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_update_ex")
@@ -491,12 +510,15 @@ class PHEngine:
         return self.x.index_select(0, idx).T.cpu().numpy()
 
     def host(self, name):
+        if name == "node_buf":
+            self._flush_xbar()
         t = getattr(self, name)
         a = t.cpu().numpy()
         return a.T if a.ndim == 2 else a
 
     def node_xbar(self):
         """{node name: x̄ vector} from the (reduced) node buffer."""
+        self._flush_xbar()
         buf = self.node_buf.cpu().numpy()
         nl = self.nlen_max
         return {nd: buf[g * nl:(g + 1) * nl] for g, nd in enumerate(self.node_names)}

@@ -116,7 +116,8 @@ class PHBase(SPOpt):
 
     # phbase.py:27-107 / 265-291
     def Compute_Xbar(self, verbose=False):
-        self.engine.compute_xbar()
+        # with one rank the engine folds x̄ into the Update_W launch (engine.compute_xbar)
+        self.engine.compute_xbar(lazy=True)
 
     # phbase.py:293-318 (fused with the x̄ scatter and the conv partial sum)
     def Update_W(self, verbose=False):

@@ -118,3 +118,48 @@ def test_update_ex_rejects_stats_before_solve(gpu):
     assert rc != 0
     e.close()
 
+
+
+@pytest.mark.parametrize("model,S,bf", [("farmer", 1000, None), ("farmer", 20000, None),
+                                        ("aircond", 128, [2, 64])])
+def test_step_local_matches_reduce_then_update(gpu, model, S, bf):
+    """phgpu_ph_step_local (one rank: x̄ folded into the update launch for two-stage
+    problems; the general route otherwise) gives the node sums, x̄, W, conv and statistics
+    of phgpu_ph_reduce + phgpu_ph_update_ex, to the last bits of the summation order."""
+    from mpisppy_amd import _lib
+    e = _engine(model, S, bf)
+    e.set_rho(1.0)
+    e.set_terms(1, 1)
+    e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
+    W0 = e.W.clone()
+    conv_a = torch.zeros(1, dtype=torch.float64).pin_memory()
+    st_a = torch.zeros(6, dtype=torch.int64).pin_memory()
+    _lib.check(e.lib.phgpu_ph_reduce(e.h, e.x.data_ptr(), e.node_buf.data_ptr(), e._stream()), "phgpu_ph_reduce")
+    _lib.check(e.lib.phgpu_ph_update_ex(e.h, e.x.data_ptr(), e.node_buf.data_ptr(), e.xbar.data_ptr(),
+                                        e.W.data_ptr(), e.rho.data_ptr(), 1, conv_a.data_ptr(), st_a.data_ptr(),
+                                        e._stream()), "phgpu_ph_update_ex")
+    torch.cuda.synchronize()
+    ref = {k: getattr(e, k).cpu().numpy().copy() for k in ("node_buf", "xbar", "W")}
+    for _ in range(2):                              # the first call may take the general route
+        e.W.copy_(W0)
+        e.node_buf.fill_(1e30)
+        conv_b = torch.zeros(1, dtype=torch.float64).pin_memory()
+        st_b = torch.zeros(6, dtype=torch.int64).pin_memory()
+        _lib.check(e.lib.phgpu_ph_step_local(e.h, e.x.data_ptr(), e.node_buf.data_ptr(), e.xbar.data_ptr(),
+                                             e.W.data_ptr(), e.rho.data_ptr(), 1, conv_b.data_ptr(),
+                                             st_b.data_ptr(), e._stream()), "phgpu_ph_step_local")
+        torch.cuda.synchronize()
+        for k, v in ref.items():
+            np.testing.assert_allclose(getattr(e, k).cpu().numpy(), v, rtol=1e-13, atol=1e-13, err_msg=k)
+        assert abs(float(conv_b[0]) - float(conv_a[0])) <= 1e-13 * abs(float(conv_a[0]))
+        assert st_b.tolist() == st_a.tolist()
+    # the PH loop's lazy path (engine.compute_xbar(lazy=True) + update) and a node_buf read
+    e.W.copy_(W0)
+    e.compute_xbar(lazy=True)
+    nb = e.host("node_buf")                          # flushes the pending x̄
+    np.testing.assert_allclose(nb, ref["node_buf"], rtol=1e-13, atol=1e-13)
+    e.compute_xbar(lazy=True)
+    e.update(True)
+    assert abs(e.convergence_diff() - float(conv_a[0])) <= 1e-13 * abs(float(conv_a[0]))
+    np.testing.assert_allclose(e.W.cpu().numpy(), ref["W"], rtol=1e-13, atol=1e-13)
+    e.close()
