@@ -1135,7 +1135,8 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
         }
     }
     acc = wave_sum(acc);
-    if ((threadIdx.x & (WAVE - 1)) == 0) cpart[s / WAVE] = acc;
+    // (the last 1,024-thread block may run past the batch's last wave: cpart has nwaves)
+    if ((threadIdx.x & (WAVE - 1)) == 0 && s / WAVE < st.nwaves) cpart[s / WAVE] = acc;
 }
 
 // spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible, prob*optimal.
