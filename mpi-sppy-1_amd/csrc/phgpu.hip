@@ -1072,7 +1072,8 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
 // node_buf; then the scatter / W update / conv partial of k_ph_update, the conv partials
 // going to their own region (cpart) because other blocks are still reading part.
 #define XL_NN_MAX 16
-#define XL_T 1024  // threads per block: every block re-sums the wave partials, so few, large blocks
+#define XL_T 1024  // threads per block at most: every block re-sums the wave partials (few, large blocks
+                   // for a large batch, phgpu_ph_step_local; 256 for a small one, to spread the update)
 __global__ void __launch_bounds__(XL_T)
 k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf,
                   double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
@@ -1087,7 +1088,7 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
     double a[XL_NN_MAX], b[XL_NN_MAX];
 #pragma unroll
     for (int k = 0; k < XL_NN_MAX; ++k) a[k] = b[k] = 0.0;
-    for (int64_t w = threadIdx.x; w < st.nwaves; w += XL_T) {
+    for (int64_t w = threadIdx.x; w < st.nwaves; w += blockDim.x) {
         const double* pw = st.part + w * nn * 2;
 #pragma unroll
         for (int k = 0; k < XL_NN_MAX; ++k)
@@ -1110,8 +1111,8 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
     if (threadIdx.x < nn) {
         const int k = threadIdx.x;
         double ta = 0.0, tb = 0.0;
-#pragma unroll
-        for (int u = 0; u < XL_T / WAVE; ++u) {
+        const int nwb = (int)(blockDim.x / WAVE);
+        for (int u = 0; u < nwb; ++u) {
             ta += sa[u][k];
             tb += sb[u][k];
         }
@@ -1135,7 +1136,7 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
         }
     }
     acc = wave_sum(acc);
-    // (the last 1,024-thread block may run past the batch's last wave: cpart has nwaves)
+    // (the last block may run past the batch's last wave: cpart has nwaves)
     if ((threadIdx.x & (WAVE - 1)) == 0 && s / WAVE < st.nwaves) cpart[s / WAVE] = acc;
 }
 
@@ -2624,8 +2625,12 @@ extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node
     }
     const size_t K = (size_t)(2 * h->nn > 5 ? 2 * h->nn : 5);
     double* cpart = h->part + (size_t)h->nwaves * K;
-    hipLaunchKernelGGL(k_ph_update_local, dim3((unsigned)((h->S + XL_T - 1) / XL_T)), dim3(XL_T), 0, st, *h, x,
-                       node_buf, xbar, W, rho, update_W ? 1 : 0, cpart);
+    // 1,024-thread blocks for a large batch (fewer re-sums of the wave partials: 10.5 us at
+    // 65,536 scenarios vs 14 us with 64-thread blocks), 256 for a small one (8,192: the update
+    // part spread over 32 blocks; profiles/r03/x/)
+    const unsigned T = h->S > 16384 ? XL_T : 256;
+    hipLaunchKernelGGL(k_ph_update_local, dim3((unsigned)((h->S + T - 1) / T)), dim3(T), 0, st, *h, x, node_buf,
+                       xbar, W, rho, update_W ? 1 : 0, cpart);
     HIPCHK(hipGetLastError());
     const double scale = 1.0 / ((double)h->S * (double)h->nn);
     hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)cpart, h->nwaves, 1, scale,
