@@ -167,7 +167,15 @@ int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
  *                spopt.py:201-206)
  *   status[S]    device out: PHGPU_* code
  *   iters[S]     device out (may be NULL): iterations used (PDHG iterations; interior-
- *                point iterations for scenarios path 6 solved)                  */
+ *                point iterations for scenarios path 6 solved)
+ * phgpu_solve_stats and phgpu_ph_update_ex(stats_out) read the status / iters outputs of
+ * the last solve launched on the handle (paths without in-kernel statistics): those
+ * buffers must stay alive until the next solve when statistics are requested.  A solve
+ * rejected by validation leaves the previous solve's buffers in place.
+ * Kernel 0 (automatic) on a pattern path 6 applies to: if its module cannot be compiled
+ * or loaded, path 6 is turned off for the handle's data (phgpu_ipm_info off = 2), the
+ * reason stays in phgpu_last_error and the solve runs on the handle's PDHG path;
+ * kernel 6 asked for explicitly returns the error instead. */
 int phgpu_solve(phgpu_handle h, const phgpu_options* opt, int warm_start, double* x,
                 double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
                 void* stream);
@@ -277,7 +285,8 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
 /* Path-6 (interior point) diagnostics: info[11] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
- * (path 6 is then not the automatic path), 1 if a module is compiled, rows in its normal
+ * and 2 if the module failed to compile or load (path 6 is then not the automatic path
+ * until new data arrives by phgpu_set_scenarios), 1 if a module is compiled, rows in its normal
  * equations, its factor entries, its scratch bytes per lane, its hipRTC compile seconds,
  * flops of one LDL' factorisation, flops of one forward + backward solve, lanes per
  * scenario of its IPM kernel (1, or a lane group of 2..16: more lanes for fewer local

@@ -2131,7 +2131,11 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     h->have_s[0] = h->have_s[1] = 0;
     h->warm_rec_s[0] = h->warm_rec_s[1] = 0;
     h->jit_kinds_valid = 0;
+    // new data: the path-6 module is specialised again at the next solve (and a spill or a
+    // failed compile of the previous data no longer decides the path)
     h->ipm_flags_valid = 0;
+    h->ipm_off = 0;
+    h->ipm_spill1 = 0;
     bind_slots(h);
     HIPCHK(run_setup(h, st));
     // the setup's start omega (slot 0) for slot 1 too
@@ -2205,9 +2209,6 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     h->wq = defer ? 1 - h->wslot : h->wslot;
     bind_slots(h);
     const int wq = h->wq;
-    h->last_stats = nullptr;  // path 6 sets it when its kernels produce the statistics
-    h->last_status = status;
-    h->last_iters = iters;
     phgpu_options o;
     if (opt) o = *opt;
     else phgpu_default_options(&o);
@@ -2270,6 +2271,9 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters);
         HIPCHK(hipGetLastError());
+        h->last_stats = nullptr;
+        h->last_status = status;
+        h->last_iters = iters;
         h->have_s[wq] = 1;
         h->last_path = 4;
         bind_slots(h);
@@ -2289,10 +2293,23 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
                        "(got %d, %d, %d, %d)", IPM_MAX_N, IPM_MAX_M, IPM_MAX_NNZ, IPM_MAX_NF, h->n, h->m, h->nnz,
                        h->ipm_nf);
     int path = o.kernel != 0 ? o.kernel : (o.gamma == 1.0 ? default_path(h) : 1);
+    // the statistics / status buffers phgpu_solve_stats and phgpu_ph_update_ex read: this
+    // solve's, once it is launched (a rejected solve leaves the previous ones)
+    unsigned long long* stats_keep = h->last_stats;
+    h->last_stats = nullptr;  // path 6 sets it when its kernels produce the statistics
     if (path == 6) {
         const int rc6 = ipm_prepare(h, st);
-        if (rc6) return rc6;
-        if (o.kernel == 0 && h->ipm->private_bytes > ipm_spill_max()) {
+        if (rc6) {
+            h->last_stats = stats_keep;
+            if (o.kernel != 0) return rc6;
+            // the automatic choice: a module that does not compile or load (a hipRTC runtime
+            // problem, an unusual pattern) turns path 6 off for this handle's data and the
+            // solve runs on the handle's PDHG path; phgpu_last_error keeps the reason and
+            // phgpu_ipm_info reports it (off = 2)
+            h->ipm_off = 2;
+            fprintf(stderr, "phgpu: path 6 unavailable (%s); solving on the PDHG path\n", g_err);
+            path = default_path(h);
+        } else if (o.kernel == 0 && h->ipm->private_bytes > ipm_spill_max()) {
             h->ipm_off = 1;  // the automatic choice falls back to the handle's PDHG path
             path = default_path(h);
         }
@@ -2443,6 +2460,8 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         out_rec = 0;
     }
     HIPCHK(hipGetLastError());
+    h->last_status = status;
+    h->last_iters = iters;
     // the warm state written by this solve; current now, or at phgpu_commit if deferred
     h->have_s[wq] = 1;
     h->warm_rec_s[wq] = out_rec;

@@ -311,7 +311,7 @@ class PHHub(Hub):
     def is_converged(self):
         # the trivial bound is a valid outer bound only when every Iter0 solve was certified
         # optimal (an ITER_LIMIT dual bound may overstate it; see PHBase.Iter0)
-        if self.opt._PHIter == 1 and getattr(self.opt, "trivial_bound_certified", True):
+        if self.opt._PHIter == 1 and getattr(self.opt, "trivial_bound_converged", True):
             self.BestOuterBound = self.OuterBoundUpdate(self.opt.trivial_bound)
         if not self.has_innerbound_spokes:
             if self.opt._PHIter == 1:

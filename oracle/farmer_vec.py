@@ -123,6 +123,22 @@ def iter0_lp(bp, sl, f0, total):
     len_o = np.where(sl_o < 0.0, np.take_along_axis(length, order, 1), 0.0)
     before = np.cumsum(len_o, axis=1) - len_o
     fill_o = np.clip(total - before, 0.0, len_o)
+    # Exact slope ties (scen0..2 with cm > 1: their crop copies have identical yields, so
+    # the optimum is a face, not a vertex): the acreage a tied group receives is split over
+    # its segments in proportion to their lengths -- for identical copies the symmetric
+    # point of the face, the solution an interior-point solve (the analytic centre) or a
+    # PDHG solve from a symmetric start converges to.  The objective is unchanged.
+    tied = (np.diff(sl_o, axis=1) == 0.0) & (len_o[:, 1:] > 0.0) & (len_o[:, :-1] > 0.0)
+    for s in np.nonzero(tied.any(1))[0]:
+        k = 0
+        while k < K * J:
+            e = k + 1
+            while e < K * J and sl_o[s, e] == sl_o[s, k] and len_o[s, e] > 0.0:
+                e += 1
+            if e - k > 1 and len_o[s, k] > 0.0:
+                tot_fill, tot_len = fill_o[s, k:e].sum(), len_o[s, k:e].sum()
+                fill_o[s, k:e] = tot_fill * len_o[s, k:e] / tot_len
+            k = e
     fill = np.empty_like(fill_o)
     np.put_along_axis(fill, order, fill_o, 1)
     x = fill.reshape(S, K, J).sum(-1)

@@ -44,6 +44,62 @@ def solve_lp_highs(A, rl, ru, lb, ub, c):
     return res.x, float(res.fun), 0
 
 
+# ------------------------------------------------------------------ HiGHS QP (stock solver)
+def solve_qp_highs(A, rl, ru, lb, ub, c, q):
+    """min c'x + 1/2 sum q x^2 s.t. rl <= Ax <= ru, lb <= x <= ub with the HiGHS QP solver
+    bundled in scipy (scipy.optimize._highspy, HiGHS 1.8.0; its active-set QP), default
+    options: the "stock solver" timing of BASELINE.md section 4.  Its x is only accurate to
+    ~4e-3 on the farmer prox QPs, so it is a timing reference, not a parity
+    oracle.  Returns (x, obj, status) with status 0 = optimal."""
+    from scipy.optimize._highspy import _core as hc
+    A = np.asarray(A, dtype=np.float64)
+    m, n = A.shape
+    csc_start, csc_index, csc_value = [0], [], []
+    for j in range(n):
+        nzr = np.nonzero(A[:, j])[0]
+        csc_index.extend(nzr.tolist())
+        csc_value.extend(A[nzr, j].tolist())
+        csc_start.append(len(csc_index))
+    inf = hc.kHighsInf
+    fin = lambda v, d: float(v) if np.isfinite(v) else d  # noqa: E731
+    lp = hc.HighsLp()
+    lp.num_col_, lp.num_row_ = n, m
+    lp.col_cost_ = np.asarray(c, dtype=np.float64)
+    lp.col_lower_ = np.array([fin(v, -inf) for v in lb])
+    lp.col_upper_ = np.array([fin(v, inf) for v in ub])
+    lp.row_lower_ = np.array([fin(v, -inf) for v in rl])
+    lp.row_upper_ = np.array([fin(v, inf) for v in ru])
+    lp.a_matrix_.format_ = hc.MatrixFormat.kColwise if hasattr(hc, "MatrixFormat") else lp.a_matrix_.format_
+    lp.a_matrix_.start_ = np.array(csc_start, dtype=np.int32)
+    lp.a_matrix_.index_ = np.array(csc_index, dtype=np.int32)
+    lp.a_matrix_.value_ = np.array(csc_value, dtype=np.float64)
+    lp.a_matrix_.num_col_, lp.a_matrix_.num_row_ = n, m
+    model = hc.HighsModel()
+    model.lp_ = lp
+    qd = np.asarray(q, dtype=np.float64)
+    nzq = np.nonzero(qd)[0]
+    if len(nzq):
+        hs = hc.HighsHessian()
+        hs.dim_ = n
+        hs.format_ = hc.HessianFormat.kTriangular
+        start = np.zeros(n + 1, dtype=np.int32)
+        for j in nzq:
+            start[j + 1:] += 1
+        hs.start_ = start
+        hs.index_ = nzq.astype(np.int32)
+        hs.value_ = qd[nzq]
+        model.hessian_ = hs
+    h = hc._Highs()
+    h.setOptionValue("output_flag", False)
+    h.passModel(model)
+    h.run()
+    st = h.getModelStatus()
+    if st != hc.HighsModelStatus.kOptimal:
+        return None, None, 1
+    x = np.array(h.getSolution().col_value)
+    return x, float(h.getInfo().objective_function_value), 0
+
+
 # ------------------------------------------------------------------ dense IPM
 def solve_qp_ipm(A, rl, ru, lb, ub, c, q, tol=1e-11, max_iter=200, polish=True):
     """min c'x + 1/2 sum q x^2 s.t. rl <= Ax <= ru, lb <= x <= ub (q >= 0).

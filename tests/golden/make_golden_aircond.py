@@ -1,6 +1,9 @@
 """Generate the config-4 scale fixture (tests/golden/aircond_scale.json).
 
 Run:  python tests/golden/make_golden_aircond.py [workers]     (~5 minutes on 8 cores)
+      python tests/golden/make_golden_aircond.py --conv [workers]
+            (aircond_conv.json: the same run continued until conv < CONV_THRESH, the
+             PH iteration count of iterk_loop's break, phbase.py:925-934)
 
 Config 4 as bench.py times it: aircond, branching factors 32 x 32 x 64 (65,536 scenarios,
 1,057 non-leaf nodes), straight_tests.py:36 parameters (Capacity 200, QuadShortCoeff 0.3,
@@ -74,9 +77,15 @@ def _solve_chunk(args):
     return np.array(xs), np.array(objs), loose
 
 
+CONV_THRESH = 1e-2     # the coarse threshold of the convergence-count fixture
+CONV_LIMIT = 80
+
+
 def main():
     from oracle.models import aircond_scenario
-    workers = int(sys.argv[1]) if len(sys.argv) > 1 else max(1, (os.cpu_count() or 2) - 1)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    to_conv = "--conv" in sys.argv
+    workers = int(args[0]) if args else max(1, (os.cpu_count() or 2) - 1)
     S = int(np.prod(BF))
     t0 = time.time()
     # tree bookkeeping (spbase.py:378-391): nonant k of scenario s belongs to node
@@ -113,7 +122,8 @@ def main():
         out = {"branching_factors": BF, "kwargs": KW, "rho": RHO, "S": S, "trivial_bound": tb,
                "sample": sample, "iter0_obj": obj[sample].tolist(), "node_names": node_names,
                "xbar": [], "conv": []}
-        for it in range(PH_ITERS):
+        n_iters = CONV_LIMIT if to_conv else PH_ITERS
+        for it in range(n_iters):
             # _Compute_Xbar (phbase.py:27-107): per node sum of prob_coeff * x, in scenario order
             nx = np.zeros((len(node_names), 2))
             for k in range(nn):
@@ -125,8 +135,29 @@ def main():
             conv = float(np.abs(x - xbar).sum() / (S * nn))          # convergence_diff (:321-343)
             out["xbar"].append(nx.tolist())
             out["conv"].append(conv)
-            x, obj = solve(True)                                     # solve_loop (:941)
             print(f"PH iteration {it + 1}: conv {conv:.10f} ({time.time() - t0:.0f}s)", flush=True)
+            if to_conv and conv < CONV_THRESH:
+                # iterk_loop breaks here, before the solve (phbase.py:925-934)
+                out["conv_thresh"] = CONV_THRESH
+                out["break_iteration"] = it + 1
+                break
+            x, obj = solve(True)                                     # solve_loop (:941)
+    if to_conv:
+        # aircond_conv.json: the PH iteration count to conv < CONV_THRESH, the conv
+        # trajectory, and x̄ of every node at the last two iterations (a run that breaks one
+        # iteration off is compared against its own iteration)
+        if "break_iteration" not in out:
+            raise RuntimeError(f"conv >= {CONV_THRESH} after {CONV_LIMIT} PH iterations")
+        conv_out = {k: out[k] for k in ("branching_factors", "kwargs", "rho", "S", "trivial_bound", "node_names",
+                                        "conv", "conv_thresh", "break_iteration")}
+        conv_out["xbar_last"] = {str(len(out["xbar"]) - k): out["xbar"][-1 - k] for k in range(min(2, len(out["xbar"])))}
+        conv_out["W_sample"] = sample
+        conv_out["W_break"] = W[sample].tolist()
+        conv_out["ipm_loose_tolerance"] = loose_all
+        with open(os.path.join(HERE, "aircond_conv.json"), "w") as f:
+            json.dump(conv_out, f)
+        print(f"done: break at {out['break_iteration']} ({time.time() - t0:.0f}s)", flush=True)
+        return
     out["ph_iters"] = PH_ITERS
     out["W"] = W[sample].tolist()
     out["Eobj"] = math.fsum(prob * obj)

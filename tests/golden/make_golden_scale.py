@@ -1,6 +1,7 @@
 """Generate the configuration-scale farmer fixtures (tests/golden/farmer_scale.json).
 
-Run:  python tests/golden/make_golden_scale.py        (~1 minute, one core)
+Run:  python tests/golden/make_golden_scale.py        (~20 minutes, one core)
+      python tests/golden/make_golden_scale.py --cm10 (config 2's set only)
       python tests/golden/make_golden_scale.py --conv (farmer_conv.json: config 3 run to
                                                        convergence, ~30 minutes)
 
@@ -13,7 +14,10 @@ Sets (SURVEY.md 8(c) "golden vectors to commit"):
   farmer65536_cm1   config 3: scen0..scen65535, cm=1, rho=1 -- trivial bound, Iter0
                     objectives and W after 5 PH iterations on every 64th scenario, x̄ and
                     conv of each of the 5 iterations, E[obj] after 5
-  farmer1024_cm10   config 2: scen0..scen1023, cm=10 -- trivial bound, sampled Iter0 objectives
+  farmer1024_cm10   config 2: scen0..scen1023, cm=10 -- trivial bound, sampled Iter0 objectives,
+                    x̄ / conv of 5 PH iterations, W of every 8th scenario and E[obj] after them;
+                    "breaks": the PH iteration at which iterk_loop stops for conv < 1e-2 and
+                    1e-3 (phbase.py:925-934), with x̄ at that iteration and its neighbours
   farmer2048_cm64   the HBM-scale variant of config 3 at test size: the first 2048
                     well-conditioned scenarios from scen3 on, cm=64, 5 PH iterations.
                     scen0..2 are skipped (with cm > 1 their crop copies tie exactly, so
@@ -117,12 +121,36 @@ def run_to_convergence(S=65536, limit=4000, stride=64):
         json.dump(out, f)
 
 
+def breaks(names, cm, thresholds=(1e-2, 1e-3), limit=3000):
+    """PH iteration counts of iterk_loop's break for each threshold, x̄ around each."""
+    ph = FarmerVecPH(names, cm, rho=1.0)
+    ph.iter0()
+    ph.iterk_loop(limit, convthresh=min(thresholds))
+    conv = [h["conv"] for h in ph.history]
+    out = {}
+    for thr in thresholds:
+        it = next(i + 1 for i, c in enumerate(conv) if c < thr)
+        out[repr(thr)] = {"iteration": it,
+                          "xbar": {str(j): ph.history[j - 1]["xbar"].tolist()
+                                   for j in (it - 1, it, it + 1) if 1 <= j <= len(conv)}}
+    return {"conv": conv, "breaks": out}
+
+
 def main():
     if "--conv" in sys.argv:
         return run_to_convergence()
+    if "--cm10" in sys.argv:  # regenerate config 2's set only
+        path = os.path.join(HERE, "farmer_scale.json")
+        out = json.load(open(path))
+        out["farmer1024_cm10"] = run([f"scen{i}" for i in range(1024)], 10, 5, 8)
+        out["farmer1024_cm10"].update(breaks([f"scen{i}" for i in range(1024)], 10))
+        with open(path, "w") as f:
+            json.dump(out, f)
+        return
     out = {}
     out["farmer65536_cm1"] = run([f"scen{i}" for i in range(65536)], 1, 5, 64)
-    out["farmer1024_cm10"] = run([f"scen{i}" for i in range(1024)], 10, 0, 8)
+    out["farmer1024_cm10"] = run([f"scen{i}" for i in range(1024)], 10, 5, 8)
+    out["farmer1024_cm10"].update(breaks([f"scen{i}" for i in range(1024)], 10))
     names64 = well_conditioned(3, 2048, 64)
     out["farmer2048_cm64"] = run(names64, 64, 5, 16)
     out["farmer2048_cm64"]["names"] = names64

@@ -146,6 +146,37 @@ def test_path6_fallback_for_every_scenario(gpu):
     assert np.abs(obj[idx] - want).max() <= OBJ_REL * np.abs(want).max()
 
 
+def test_path6_compile_failure_falls_back_to_the_pdhg_path(gpu):
+    """A path-6 module that does not compile (here a broken macro definition injected by
+    PHGPU_IPM_DEFS): the automatic choice turns path 6 off for the handle and solves on
+    the handle's PDHG path with the same answers; kernel 6 asked for explicitly raises."""
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd import _lib
+    S = 256
+    b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=1, num_scens=S)
+    ref = PHEngine(b, device="cuda:0")
+    ref.solve(_lib.default_options(kernel=2, eps_rel=1e-10), warm=False)
+    want = ref.host("obj").copy()
+    ref.close()
+    keep = os.environ.get("PHGPU_IPM_DEFS")
+    os.environ["PHGPU_IPM_DEFS"] = "IPM_SIG_MAX=(0.05"   # unbalanced parenthesis: hipRTC fails
+    try:
+        e = PHEngine(b, device="cuda:0")
+        with pytest.raises(_lib.PhgpuError):
+            e.solve(_lib.default_options(kernel=6, eps_rel=1e-10), warm=False)
+        e.solve(_lib.default_options(eps_rel=1e-10), warm=False)
+        assert (e.host("status") == 0).all()
+        assert e.ipm_info()["off"] == 2 and e.kernel_info()["path"] in (2, 5), (e.ipm_info(), e.kernel_info())
+        assert np.abs(e.host("obj") - want).max() <= OBJ_REL * np.abs(want).max()
+        e.close()
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_IPM_DEFS", None)
+        else:
+            os.environ["PHGPU_IPM_DEFS"] = keep
+
+
 def test_path6_fixed_nonants_match_register_path(gpu):
     """Xhat-style evaluation: nonants fixed per scenario (phgpu_fix_nonants) on path 6 and
     on the register path give the same objectives; restoring the bounds restores the LP."""

@@ -77,12 +77,41 @@ def test_headline_farmer65536_cm1_register_path(gpu, register_path):
     assert ph.engine.kernel_info()["rec"] == 1
 
 
+def _bench_path(ph):
+    """The kernel path of the handle's last solve (phgpu_kernel_info)."""
+    return ph.engine.kernel_info()["path"]
+
+
 def test_config2_farmer1024_cm10_bound(gpu):
-    """Config 2: trivial bound and sampled Iter0 objectives of scen0..scen1023 at cm = 10."""
+    """Config 2 on the path bench.py times (the automatic choice): trivial bound, sampled
+    Iter0 objectives, x̄ and conv of 5 PH iterations, every 8th scenario's W and E[obj]
+    after them, for scen0..scen1023 at cm = 10."""
     g = SCALE["farmer1024_cm10"]
+    assert g["ph_iters"] == 5
     names = [f"scen{i}" for i in range(1024)]
-    ph = _farmer_ph(names, 10, 1024)
+    from mpisppy_amd.examples import farmer
+    ph = _farmer_ph(names, 10, 1024, iterk_solver_options=dict(farmer.PDHG_ITERK_OPTIONS))
     _run_and_compare(ph, g)
+    print("config 2 path", _bench_path(ph), ph.engine.kernel_info())
+
+
+@pytest.mark.parametrize("thr", ["0.01"])
+def test_config2_ph_iterations_to_convergence(gpu, thr):
+    """Config 2 run by ph_main to conv < thr: iterk_loop breaks at the oracle's PH
+    iteration +-1 (phbase.py:925-934), with x̄ at that iteration within 1e-5."""
+    g = SCALE["farmer1024_cm10"]
+    want = g["breaks"][thr]
+    names = [f"scen{i}" for i in range(1024)]
+    from mpisppy_amd.examples import farmer
+    ph = _farmer_ph(names, 10, 1024, iters=want["iteration"] + 20,
+                    iterk_solver_options=dict(farmer.PDHG_ITERK_OPTIONS))
+    ph.options["convthresh"] = float(thr)
+    ph.ph_main()
+    assert ph.converged
+    assert abs(ph._PHIter - want["iteration"]) <= 1, (ph._PHIter, want["iteration"])
+    xb = ph.xbar_by_node()["ROOT"][:30]
+    ref = np.array(want["xbar"][str(ph._PHIter)])
+    assert np.abs(xb - ref).max() <= ABS, np.abs(xb - ref).max()
 
 
 def test_headline_instance_on_a_slice(gpu, register_path):

@@ -43,6 +43,25 @@ def extract_group(nm):
     return int(nm[4:]) // 3
 
 
+@pytest.mark.parametrize("cm", [2, 10])
+def test_vec_lp_tied_copies_take_the_symmetric_point(cm):
+    """scen0..2 at cm > 1: every copy of a crop has the same yields, the Iter0 optimum is a
+    face; the oracle takes its symmetric point (equal acreage per copy), which is feasible
+    and optimal (HiGHS objective) and equals cm copies of the cm = 1 solution scaled."""
+    warnings.simplefilter("ignore")
+    names = ["scen0", "scen1", "scen2"]
+    bp, sl, f0 = fv.pieces(fv.yields(names, cm), cm)
+    x, obj = fv.iter0_lp(bp, sl, f0, 500.0 * cm)
+    bp1, sl1, f01 = fv.pieces(fv.yields(names, 1), 1)
+    x1, obj1 = fv.iter0_lp(bp1, sl1, f01, 500.0)
+    bases = [c.rstrip("0123456789") for c in fv.crops_sorted(cm)]
+    for s in range(3):
+        for k, b in enumerate(bases):
+            assert abs(x[s, k] - x1[s, fv.crops_sorted(1).index(b + "0")]) <= 1e-9, (s, k)
+        assert abs(obj[s] - cm * obj1[s]) <= 1e-9 * abs(obj[s])
+        assert x[s].sum() <= 500.0 * cm + 1e-9
+
+
 @pytest.mark.parametrize("cm", [1, 10])
 def test_vec_prox_matches_exact(cm):
     names = [f"scen{i}" for i in range(3, 23)]
