@@ -215,9 +215,13 @@ int phgpu_ph_update(phgpu_handle h, const double* x, const double* node_buf, dou
 /* phgpu_ph_update, plus: stats_out (int64[6], may be NULL) receives the statistics of
  * the handle's last solve launch as phgpu_solve_stats reports them, written by the same
  * kernel that writes conv_local.  conv_local and stats_out may be host-mapped pinned
- * memory (zero-copy: the host reads them after an event recorded behind this call),
- * which saves the copy launches of the PH loop's convergence and gripe readbacks
- * (phbase.py:330-343, spopt.py:284-294).  Clears no other state. */
+ * memory (zero-copy), which saves the copy launches of the PH loop's convergence and gripe
+ * readbacks (phbase.py:330-343, spopt.py:284-294): the host may read them after an event
+ * recorded behind this call, or poll them -- they are written last, by one store
+ * instruction, so a caller that set conv_local to NaN and stats_out to -1 before the call
+ * has all seven values once none of them is a sentinel (the engine does that: no event
+ * marker in the PH step).  The conv reduction over the grid is done by the kernel's last
+ * block.  Clears no other state. */
 int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double* node_buf, double* xbar,
                        double* W, const double* rho, int update_W, double* conv_local,
                        int64_t* stats_out, void* stream);

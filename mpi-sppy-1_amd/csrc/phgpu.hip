@@ -30,6 +30,9 @@
 #define WAVE 64
 #define BLOCK 64
 #define ORDER_BINS 256  // counting-sort bins of the longest-first work queue (solve_reg.inc)
+#define XL_T 1024        // threads per block of k_ph_update_local at most
+#define XL_NN_MAX 16     // nonants per scenario at most for the folded x̄ paths (k_ph_update_local, IPM epilogues)
+#define XP_CHUNK_MIN 16  // smallest x̄-partial chunk of the IPM epilogues (256 / 16 lanes)
 
 // ------------------------------------------------------------------ errors
 static thread_local char g_err[512] = {0};
@@ -163,6 +166,17 @@ struct phgpu_state {
     // (null: compute on request)
     unsigned long long *ipm_stats, *stats_gen, *last_stats;
     const int32_t *last_status, *last_iters;
+    // x̄ partial sums written by the path-6 kernels' epilogue, per warm slot:
+    // [chunks * nn * 2] sums of pcoef x and pcoef x^2, node tags [chunks * nn], fallback
+    // flags [chunks]; valid for the x buffer xp_x[slot] when xp_C[slot] (the chunk size) > 0
+    double* xp[2];
+    int32_t *xp_node[2], *xp_dirty[2];
+    const double* xp_x[2];
+    int xp_C[2];
+    int64_t xp_n[2];
+    // the update kernels' last-block reduction of conv: per-block partials and a counter
+    double* cpart_blk;
+    int32_t* blk_cnt;
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -934,8 +948,25 @@ __global__ void __launch_bounds__(BLOCK) k_xbar_mixed(phgpu_state st, int32_t* _
 // that lies inside one thread's chunk of waves is complete and is flushed directly;
 // the first / last run of every chunk go through shared memory and thread 0 merges
 // them in chunk order (deterministic for every wave-uniform node).
+// x̄ partial of nonant k over chunk w recomputed from x (a chunk of the path-6 epilogue
+// partials with a scenario the fallback solved), in scenario order
+__device__ __forceinline__ void xp_recompute(const phgpu_state& st, const double* __restrict__ x, int64_t w, int C,
+                                             int k, double& a, double& b) {
+    const int64_t S = st.S;
+    const int d = st.nonant_depth[k], j = st.nonant_col[k];
+    const int64_t s1 = (w + 1) * C < S ? (w + 1) * C : S;
+    a = b = 0.0;
+    for (int64_t s = w * C; s < s1; ++s) {
+        const double p = st.pcoef[IX(d)], v = x[IX(j)];
+        a += p * v;
+        b += p * v * v;
+    }
+}
+
 #define XF_THREADS 256
-__global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, double* __restrict__ node_buf) {
+__global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, double* __restrict__ node_buf,
+                                                           const int32_t* __restrict__ dirty = nullptr,
+                                                           int xpC = 0, const double* __restrict__ x = nullptr) {
     __shared__ int fnode[XF_THREADS], lnode[XF_THREADS];
     __shared__ double fa[XF_THREADS], fb[XF_THREADS], la[XF_THREADS], lb[XF_THREADS];
     const int k = blockIdx.x;
@@ -965,8 +996,15 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
             a = 0.0;
             b = 0.0;
         }
-        a += st.part[(w * st.nn + k) * 2 + 0];
-        b += st.part[(w * st.nn + k) * 2 + 1];
+        if (dirty && dirty[w]) {
+            double ra, rb;
+            xp_recompute(st, x, w, xpC, k, ra, rb);
+            a += ra;
+            b += rb;
+        } else {
+            a += st.part[(w * st.nn + k) * 2 + 0];
+            b += st.part[(w * st.nn + k) * 2 + 1];
+        }
     }
     if (first < 0) {  // zero or one run in this chunk: it is the first (and last) run
         fnode[t] = cur;
@@ -1043,11 +1081,66 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
     }
 }
 
-// phbase.py:90-103 (scatter x̄), 293-318 (W update), 330-339 (local |x - x̄| sum).
-__global__ void __launch_bounds__(BLOCK)
+// Where the update kernels leave conv (phbase.py:330-339) and the last solve's statistics
+struct conv_sink {
+    double* conv;                          // conv_local (pinned host or device memory)
+    const unsigned long long* stats_src;   // the last solve's statistics (device), or null
+    int64_t* stats_dst;                    // where they go (pinned host or device), or null
+    double scale;                          // 1 / (S nn)
+    double* cpart;                         // [gridDim.x] block partials
+    int32_t* cnt;                          // last-block counter (0 between launches)
+};
+
+// conv = scale x (sum over the grid of every thread's acc), without a second launch: each
+// block reduces its threads in a fixed order and swaps its partial into cpart[block], then
+// takes a ticket; the block with the last ticket sums cpart in block order (deterministic)
+// and stores the statistics, then conv.  Every cross-block exchange is an agent-scope atomic
+// read-modify-write, performed at the device's coherence point, so no block needs a release
+// fence (an L2 writeback on gfx950); the ticket is taken only after the swap
+// has returned.  The host reads stats after it sees conv (phgpu_ph_update_ex).
+__device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) {
+    __shared__ double red[XL_T / WAVE];
+    __shared__ int last;
+    const int wv = threadIdx.x / WAVE, nwb = (int)(blockDim.x / WAVE);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & (WAVE - 1)) == 0) red[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int u = 0; u < nwb; ++u) t += red[u];
+        const double old = __hip_atomic_exchange(&o.cpart[blockIdx.x], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old) : "memory");  // the swap has returned before the ticket
+        const int tk = __hip_atomic_fetch_add(o.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = tk == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    double a = 0.0;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x)
+        a += __hip_atomic_fetch_add(&o.cpart[b], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a = wave_sum(a);
+    __syncthreads();
+    if ((threadIdx.x & (WAVE - 1)) == 0) red[wv] = a;
+    __syncthreads();
+    // lanes 0..5 store the statistics and lane 6 conv in one store instruction (no wait for
+    // the host-memory acknowledgements: the host polls conv and the statistics' sentinels,
+    // engine.convergence_wait)
+    if (threadIdx.x < WAVE) {
+        double t = 0.0;
+        for (int u = 0; u < nwb; ++u) t += red[u];
+        if (threadIdx.x < 6 && o.stats_dst) o.stats_dst[threadIdx.x] = (int64_t)o.stats_src[threadIdx.x];
+        if (threadIdx.x == 6) *o.conv = t * o.scale;
+        if (threadIdx.x == 0) __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// phbase.py:90-103 (scatter x̄), 293-318 (W update), 330-339 (local |x - x̄| sum, reduced
+// by the last block into conv_local).
+#define UPD_T 256
+__global__ void __launch_bounds__(UPD_T)
 k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restrict__ node_buf,
             double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
-            int update_W) {
+            int update_W, conv_sink o) {
     const int64_t S = st.S;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double acc = 0.0;
@@ -1062,22 +1155,20 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
             acc += fabs(xv - xb);
         }
     }
-    acc = wave_sum(acc);
-    if ((threadIdx.x & (WAVE - 1)) == 0) st.part[s / WAVE] = acc;
+    conv_last_block(acc, o);
 }
 
 // phgpu_ph_step_local (one rank, every nonant's scenarios on one node, nn <= XL_NN_MAX):
 // k_xbar_final and k_ph_update in one launch.  Every block sums the per-wave x̄ partials
 // itself, in one fixed order (so every block gets the same bits), block 0 stores them in
-// node_buf; then the scatter / W update / conv partial of k_ph_update, the conv partials
-// going to their own region (cpart) because other blocks are still reading part.
-#define XL_NN_MAX 16
-#define XL_T 1024  // threads per block at most: every block re-sums the wave partials (few, large blocks
-                   // for a large batch, phgpu_ph_step_local; 256 for a small one, to spread the update)
+// node_buf; then the scatter / W update / conv of k_ph_update (last-block reduction).  The
+// partials are per wave (k_xbar_partial) or per chunk of the path-6 epilogue (st.part /
+// st.nwaves then point at those; dirty chunks are recomputed from x).  Few, large blocks for
+// a large batch (every block re-sums the partials), 256 threads for a small one.
 __global__ void __launch_bounds__(XL_T)
 k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restrict__ node_buf,
                   double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
-                  int update_W, double* __restrict__ cpart) {
+                  int update_W, conv_sink o, const int32_t* __restrict__ dirty, int C) {
     __shared__ double sa[XL_T / WAVE][XL_NN_MAX], sb[XL_T / WAVE][XL_NN_MAX];
     __shared__ double xbs[XL_NN_MAX];
     const int64_t S = st.S;
@@ -1090,6 +1181,16 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
     for (int k = 0; k < XL_NN_MAX; ++k) a[k] = b[k] = 0.0;
     for (int64_t w = threadIdx.x; w < st.nwaves; w += blockDim.x) {
         const double* pw = st.part + w * nn * 2;
+        if (dirty && dirty[w]) {  // a chunk with a fallback scenario (path-6 partials)
+            for (int k = 0; k < nn; ++k) {
+                double ra, rb;
+                xp_recompute(st, x, w, C, k, ra, rb);
+#pragma unroll
+                for (int u = 0; u < XL_NN_MAX; ++u)
+                    if (u == k) a[u] += ra, b[u] += rb;
+            }
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < XL_NN_MAX; ++k)
             if (k < nn) {
@@ -1135,9 +1236,7 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
             acc += fabs(xv - xb);
         }
     }
-    acc = wave_sum(acc);
-    // (the last block may run past the batch's last wave: cpart has nwaves)
-    if ((threadIdx.x & (WAVE - 1)) == 0 && s / WAVE < st.nwaves) cpart[s / WAVE] = acc;
+    conv_last_block(acc, o);
 }
 
 // spopt.py:310-439 local sums: prob*obj, prob*bound, prob, prob*feasible, prob*optimal.
@@ -1812,6 +1911,22 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         size_t K = (size_t)(2 * nn > 5 ? 2 * nn : 5);
         ALLOC(h->part, (size_t)h->nwaves * (K + 1));
         ALLOC(h->part_node, (size_t)h->nwaves * (nn > 0 ? nn : 1));
+        // path-6 epilogue partials (two slots) and the update kernels' conv partials (one
+        // per block of the widest update grid: 64 lanes per block at least)
+        if (!h->shared && h->ipm_nf > 0 && nn > 0 && nn <= XL_NN_MAX) {
+            const size_t nch = (Sz + XP_CHUNK_MIN - 1) / XP_CHUNK_MIN;
+            for (int k = 0; k < 2; ++k) {
+                ALLOC(h->xp[k], nch * 2 * (size_t)nn);
+                ALLOC(h->xp_node[k], nch * (size_t)nn);
+                ALLOC(h->xp_dirty[k], nch);
+            }
+        }
+        ALLOC(h->cpart_blk, (Sz + BLOCK - 1) / BLOCK + 1);
+        ALLOC(h->blk_cnt, 4);
+        if (hipMemset(h->blk_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess) {
+            phgpu_destroy(h);
+            return set_err(-2, "hipMemset failed");
+        }
     }
     (void)rc;
     hipError_t e = hipSuccess;
@@ -2462,6 +2577,7 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     HIPCHK(hipGetLastError());
     h->last_status = status;
     h->last_iters = iters;
+    if (path != 6) h->xp_C[wq] = 0;  // only path 6 writes x̄ partials with its outputs
     // the warm state written by this solve; current now, or at phgpu_commit if deferred
     h->have_s[wq] = 1;
     h->warm_rec_s[wq] = out_rec;
@@ -2577,16 +2693,56 @@ static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipS
     return 0;
 }
 
+// the path-6 epilogue partials of x when the last solve writing the current slot produced
+// them for this x buffer, else null
+static bool xp_valid(const phgpu_state* h, const double* x) {
+    const int k = h->wslot;
+    return h->xp[k] && h->xp_C[k] > 0 && h->xp_x[k] == x && h->xbar_mixed == 0;
+}
+static phgpu_state xp_view(const phgpu_state* h) {  // the state with part = the epilogue partials
+    phgpu_state v = *h;
+    v.part = h->xp[h->wslot];
+    v.part_node = h->xp_node[h->wslot];
+    v.nwaves = h->xp_n[h->wslot];
+    return v;
+}
+
 extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
     if (!h || !x || !node_buf) return set_err(-1, "null argument");
     hipStream_t st = (hipStream_t)stream;
     const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
     if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
                                ? 0 : set_err(-2, "hipMemsetAsync failed");
+    if (xp_valid(h, x)) {
+        // the solve's epilogue wrote the per-chunk partials: clear node_buf, final sums
+        HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
+        hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, xp_view(h), node_buf,
+                           (const int32_t*)h->xp_dirty[h->wslot], h->xp_C[h->wslot], x);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     const int rc = xbar_partials(h, x, node_buf, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf);
+    hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, *h, node_buf, nullptr, 0, nullptr);
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// the conv / statistics sink of the update kernels; launches k_solve_stats first when the
+// last solve's path has no in-kernel statistics
+static int make_sink(phgpu_state* h, double* conv_local, int64_t* stats_out, hipStream_t st, conv_sink& o) {
+    o.conv = conv_local;
+    o.stats_dst = stats_out;
+    o.stats_src = stats_out ? h->last_stats : nullptr;
+    if (stats_out && !o.stats_src) {  // a path without in-kernel statistics
+        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
+                           h->stats_gen);
+        HIPCHK(hipGetLastError());
+        o.stats_src = h->stats_gen;
+    }
+    o.scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
+    o.cpart = h->cpart_blk;
+    o.cnt = h->blk_cnt;
     return 0;
 }
 
@@ -2597,19 +2753,12 @@ extern "C" int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double*
         return set_err(-1, "null argument");
     if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_update_ex: stats_out before any solve");
     hipStream_t st = (hipStream_t)stream;
-    const unsigned long long* src = stats_out ? h->last_stats : nullptr;
-    if (stats_out && !src) {  // a path without in-kernel statistics
-        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
-                           h->stats_gen);
-        HIPCHK(hipGetLastError());
-        src = h->stats_gen;
-    }
-    hipLaunchKernelGGL(k_ph_update, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, xbar, W, rho,
-                       update_W ? 1 : 0);
-    HIPCHK(hipGetLastError());
-    const double scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
-    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)h->part, h->nwaves, 1,
-                       scale, conv_local, src, stats_out);
+    conv_sink o;
+    const int rc = make_sink(h, conv_local, stats_out, st, o);
+    if (rc) return rc;
+    // one launch: x̄ scatter, W update, conv (last-block reduction) and the statistics
+    hipLaunchKernelGGL(k_ph_update, dim3((unsigned)((h->S + UPD_T - 1) / UPD_T)), dim3(UPD_T), 0, st, *h, x,
+                       node_buf, xbar, W, rho, update_W ? 1 : 0, o);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2633,27 +2782,23 @@ extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node
         if (rc) return rc;
         return phgpu_ph_update_ex(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, stream);
     }
-    const int rc = xbar_partials(h, x, node_buf, st);
-    if (rc) return rc;
-    const unsigned long long* src = stats_out ? h->last_stats : nullptr;
-    if (stats_out && !src) {
-        hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
-                           h->stats_gen);
-        HIPCHK(hipGetLastError());
-        src = h->stats_gen;
+    // the per-chunk x̄ partials: from the path-6 epilogue when it wrote them for this x,
+    // else from k_xbar_partial
+    const bool xp = xp_valid(h, x);
+    if (!xp) {
+        const int rc = xbar_partials(h, x, node_buf, st);
+        if (rc) return rc;
     }
-    const size_t K = (size_t)(2 * h->nn > 5 ? 2 * h->nn : 5);
-    double* cpart = h->part + (size_t)h->nwaves * K;
-    // 1,024-thread blocks for a large batch (fewer re-sums of the wave partials: 10.5 us at
+    conv_sink o;
+    const int rc = make_sink(h, conv_local, stats_out, st, o);
+    if (rc) return rc;
+    // 1,024-thread blocks for a large batch (fewer re-sums of the partials: 10.5 us at
     // 65,536 scenarios vs 14 us with 64-thread blocks), 256 for a small one (8,192: the update
     // part spread over 32 blocks; profiles/r03/x/)
     const unsigned T = h->S > 16384 ? XL_T : 256;
-    hipLaunchKernelGGL(k_ph_update_local, dim3((unsigned)((h->S + T - 1) / T)), dim3(T), 0, st, *h, x, node_buf,
-                       xbar, W, rho, update_W ? 1 : 0, cpart);
-    HIPCHK(hipGetLastError());
-    const double scale = 1.0 / ((double)h->S * (double)h->nn);
-    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, (const double*)cpart, h->nwaves, 1, scale,
-                       conv_local, src, stats_out);
+    hipLaunchKernelGGL(k_ph_update_local, dim3((unsigned)((h->S + T - 1) / T)), dim3(T), 0, st,
+                       xp ? xp_view(h) : *h, x, node_buf, xbar, W, rho, update_W ? 1 : 0, o,
+                       xp ? (const int32_t*)h->xp_dirty[h->wslot] : nullptr, xp ? h->xp_C[h->wslot] : 0);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2723,6 +2868,12 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
     if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
     if (h->ipm_stats) (void)hipFree(h->ipm_stats);
     if (h->stats_gen) (void)hipFree(h->stats_gen);
+    {
+        void* more[] = {h->xp[0], h->xp[1], h->xp_node[0], h->xp_node[1], h->xp_dirty[0], h->xp_dirty[1],
+                        h->cpart_blk, h->blk_cnt};
+        for (void* p : more)
+            if (p) (void)hipFree(p);
+    }
     if (!h->shared) {  // warm-start slot 1 (slot 0 is x / y / omega / sk_iters above)
         void* slot1[] = {h->xs[1], h->ys[1], h->oms[1], h->its_s[1]};
         for (void* p : slot1)

@@ -133,14 +133,21 @@ class PHEngine:
         self._row_of = {}
         self._stats_rows = torch.zeros((1, 6), dtype=torch.int64).pin_memory()
         self._stats_tmp = torch.zeros(6, dtype=torch.int64).pin_memory()
-        self._conv_host = torch.zeros(1, dtype=torch.float64).pin_memory()
+        # conv readback: the update kernel (one rank) or the copy behind the conv all-reduce
+        # (several ranks) stores conv into this pinned word, which the host set to NaN before
+        # the update was queued; the host polls it -- no event marker in the PH step (each
+        # marker is a barrier packet that idles the GPU ~5.6 us)
+        self._conv_host = torch.full((1,), float("nan"), dtype=torch.float64).pin_memory()
+        self._conv_np = self._conv_host.numpy()
         self._conv_zero_copy = False
-        # markers: the event behind each update (by update number), recorded lazily -- every
-        # event record is a barrier packet that idles the GPU ~5 us, so one PH step records
-        # one (the instrumented bench shares it with its solve-start timing event)
+        self._conv_seq = 0        # the update whose conv the pending readback returns
+        self._conv_seen = 0       # the last update whose conv (and statistics) the host has seen
+        self._side = None         # side stream of the conv all-reduce (several ranks)
+        self._wait_stats = None   # the pinned statistics row the pending update writes (one rank)
+        # markers: the event behind an update (by update number), recorded lazily, only when
+        # the host needs an update's statistics before its conv arrived
         self._upd_seq = 0
         self._upd_marks = {}
-        self._conv_ev = None
         self._upload()
 
     # -------------------------------------------------------------- plumbing
@@ -216,14 +223,15 @@ class PHEngine:
     # -------------------------------------------------------------- instrumentation
     _AR_TIMED = 8
 
-    def instrument(self, max_solves):
-        """Record the next ``max_solves`` phgpu_solve launches: HIP events on the launch
-        stream around each launch (the start event doubles as the update's marker the host
-        waits on for conv) and the launch's statistics (status counts, iteration sum and
-        maximum; written to pinned memory by the next update kernel, the last launch's by
-        phgpu_solve_stats).  Used by bench.py for the per-launch roofline inside its timed
-        region."""
-        self._ins = {"events": [], "ids": [], "max": int(max_solves), "ar_events": [], "ar_count": 0,
+    def instrument(self, max_solves, every=1):
+        """Record every ``every``-th of the next ``max_solves`` phgpu_solve launches: HIP
+        events on the launch stream around the launch and its statistics (status counts,
+        iteration sum and maximum; written to pinned memory by the next update kernel, the
+        last launch's by phgpu_solve_stats).  Used by bench.py for the per-launch roofline
+        inside its timed region; each event is a marker packet that idles the GPU ~5.6 us,
+        so the bench samples one step in ``every``."""
+        self._ins = {"events": [], "ids": [], "max": int(max_solves), "every": max(1, int(every)), "seen": 0,
+                     "ar_events": [], "ar_count": 0,
                      "rows": torch.zeros((max_solves + 4, 6), dtype=torch.int64).pin_memory(), "next": 0}
 
     def instrumented(self):
@@ -250,8 +258,9 @@ class PHEngine:
         return out
 
     def _recording(self):
+        """True while instrumenting (the next ``max_solves`` solves)."""
         ins = getattr(self, "_ins", None)
-        return ins is not None and len(ins["events"]) < ins["max"]
+        return ins is not None and ins["seen"] < ins["max"]
 
     def _marker(self, seq=None):
         """The event behind update ``seq`` (default: the last one), recorded now if it has
@@ -269,7 +278,8 @@ class PHEngine:
         where = self._row_of.get(lid)
         if where is not None:
             rows, r, seq = where
-            self._marker(seq).synchronize()
+            if seq > self._conv_seen:   # the update's conv (written after them) not seen yet
+                self._marker(seq).synchronize()
             return rows[r].clone()
         if lid == self._launch_id and lid:
             _lib.check(self.lib.phgpu_solve_stats(self.h, _ptr(self._stats_tmp), self._stream()), "phgpu_solve_stats")
@@ -277,22 +287,26 @@ class PHEngine:
             return self._stats_tmp.clone()
         return None
 
-    def instrumented_allreduce_ms(self):
+    def instrumented_allreduce_ms(self, tag=None):
         """Total ms of the x̄ / conv all-reduces issued while instrumenting (HIP events on
-        the current stream around each collective; 0 with one rank, where they are no-ops)."""
+        the issuing stream around each collective; 0 with one rank, where they are no-ops);
+        ``tag`` "critical" / "overlapped" selects the x̄ or the conv ones."""
         ins = getattr(self, "_ins", None)
         if not ins:
             return 0.0
         torch.cuda.synchronize(self.device)
-        if not ins["ar_events"]:
+        evs = [(ev, t) for ev, t in ins["ar_events"] if tag is None or t == tag]
+        if not evs or not ins["ar_events"]:
             return 0.0
-        mean = sum(a.elapsed_time(b) for a, b in ins["ar_events"]) / len(ins["ar_events"])
-        return float(mean * ins["ar_count"])
+        mean = sum(a.elapsed_time(b) for (a, b), _ in evs) / len(evs)
+        return float(mean * ins["ar_count"] * len(evs) / len(ins["ar_events"]))
 
-    def _allreduce_sum_(self, t):
-        """comm.allreduce_sum_ with HIP events around it while instrumenting."""
+    def _allreduce_sum_(self, t, tag="critical"):
+        """comm.allreduce_sum_ with HIP events around it while instrumenting (``tag``:
+        "critical", ahead of the next solve on the launch stream, or "overlapped", the conv
+        all-reduce on the side stream)."""
         ins = getattr(self, "_ins", None)
-        if ins is None or self.comm.size == 1 or len(ins["events"]) >= ins["max"]:
+        if ins is None or self.comm.size == 1 or not self._recording():
             return self.comm.allreduce_sum_(t)
         # the first _AR_TIMED all-reduces are timed (each event record is a marker packet
         # that idles the GPU ~5.6 us); the rest are counted and the mean extrapolated
@@ -303,7 +317,7 @@ class PHEngine:
         ev[0].record()
         self.comm.allreduce_sum_(t)
         ev[1].record()
-        ins["ar_events"].append(ev)
+        ins["ar_events"].append((ev, tag))
         return t
 
     # -------------------------------------------------------------- hot path
@@ -325,7 +339,10 @@ class PHEngine:
         else:
             out = {k: getattr(self, k) for k in self._OUTS}
         ins = getattr(self, "_ins", None)
-        rec = self._recording()
+        rec = False
+        if self._recording():
+            rec = ins["seen"] % ins["every"] == 0
+            ins["seen"] += 1
         if rec:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -416,6 +433,7 @@ class PHEngine:
         them there)."""
         self._conv_zero_copy = self.comm.size == 1
         conv = self._conv_host if self._conv_zero_copy else self.conv_buf
+        self._conv_np[0] = float("nan")     # the readback's sentinel (before the launch)
         self._upd_seq += 1
         self._upd_marks = {k: v for k, v in self._upd_marks.items() if k > self._upd_seq - 4}
         self._upd_marks[self._upd_seq] = None
@@ -430,6 +448,8 @@ class PHEngine:
                 self._row_of = {k: v for k, v in self._row_of.items() if v[0] is not rows}
             self._row_of[self._launch_id] = (rows, r, self._upd_seq)
             stats = rows[r]
+            rows.numpy()[r] = -1            # the statistics' sentinels (convergence_wait)
+        self._wait_stats = stats.numpy() if (stats is not None and self._conv_zero_copy) else None
         if getattr(self, "_xbar_pending", False):
             self._xbar_pending = False
             _lib.check(self.lib.phgpu_ph_step_local(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
@@ -442,30 +462,46 @@ class PHEngine:
 
     def convergence_diff(self):
         """phbase.py:330-343: sum over ranks of per-rank means, / n_proc (host float)."""
-        if self._conv_zero_copy:
-            self._marker().synchronize()
-            return float(self._conv_host[0])
-        self._allreduce_sum_(self.conv_buf)
-        return float(self.conv_buf.item()) / self.comm.size
+        self.convergence_diff_async()
+        return self.convergence_wait()
 
     def convergence_diff_async(self):
-        """Start the same readback without waiting (an event behind the update's host
-        write, or the all-reduce and a pinned copy): ``convergence_wait`` returns it; work
-        queued after this call does not delay it."""
+        """Start the same readback without waiting; ``convergence_wait`` returns it and work
+        queued after this call does not delay it.  One rank: the update kernel stores conv
+        into pinned memory itself.  Several ranks: the conv all-reduce (phbase.py:341) and
+        its copy into pinned memory run on a side stream behind the update, so the next
+        solve launches at once and only the x̄ all-reduce stays ahead of it."""
+        self._conv_seq = self._upd_seq
         if self._conv_zero_copy:
-            # the update's marker; while instrumenting, the next solve's start event
-            self._conv_ev = None if self._recording() else self._marker()
-            self._conv_seq = self._upd_seq
             return
-        self._allreduce_sum_(self.conv_buf)
-        self._conv_host.copy_(self.conv_buf, non_blocking=True)
-        self._conv_ev = torch.cuda.Event()
-        self._conv_ev.record()
+        main = torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        self._upd_marks[self._upd_seq] = ev        # (also the update's marker for its stats)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            self._allreduce_sum_(self.conv_buf, tag="overlapped")
+            self._conv_host.copy_(self.conv_buf, non_blocking=True)
+
+    _SPIN = 200000
 
     def convergence_wait(self):
-        ev = self._conv_ev if self._conv_ev is not None else self._marker(self._conv_seq)
-        ev.synchronize()
-        return float(self._conv_host[0]) / self.comm.size
+        """The pending conv (polls the pinned word; after a long wait it synchronises the
+        streams, which also surfaces a device error)."""
+        a = self._conv_np
+        st = self._wait_stats if self._conv_zero_copy else None
+        n = 0
+        while a[0] != a[0] or (st is not None and (st == -1).any()):
+            n += 1
+            if n > self._SPIN:
+                torch.cuda.current_stream(self.device).synchronize()
+                if self._side is not None:
+                    self._side.synchronize()
+                break
+        self._conv_seen = max(self._conv_seen, self._conv_seq)
+        return float(a[0]) / self.comm.size
 
     def expectations(self):
         """(Eobj, Ebound, E1, Efeas, Eoptimal) summed over ranks (spopt.py:310-439)."""

@@ -34,6 +34,9 @@ static inline unsigned long long atomicMax(unsigned long long* p, unsigned long 
 static inline unsigned long long __ballot(bool b) { return b ? 1ull : 0ull; }
 static inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 template <class T> static inline T __shfl_xor(T, int, int) { return T(0); }  // one lane: the others contribute 0
+template <class T> static inline T __shfl_down(T, int, int) { return T(0); }
+template <class T> static inline T __shfl(T v, int, int) { return v; }
+static inline bool __any(bool b) { return b; }
 """
 
 DRIVER = r"""
@@ -78,7 +81,9 @@ class _Params(ctypes.Structure):
                                   "status", "iters", "fail_list", "fail_n", "zero3")]
                 + [("S", ctypes.c_longlong), ("W_on", ctypes.c_int), ("prox_on", ctypes.c_int),
                    ("eps_rel", ctypes.c_double), ("eps_abs", ctypes.c_double), ("eps_tight", ctypes.c_double),
-                   ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP)])
+                   ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP),
+                   # x̄ partials of the epilogue (null here: the host run skips them)
+                   ("xp", _VP), ("xp_node", _VP), ("xp_dirty", _VP), ("pcoef", _VP), ("node_of", _VP)])
 
 
 def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13,

@@ -163,3 +163,54 @@ def test_step_local_matches_reduce_then_update(gpu, model, S, bf):
     assert abs(e.convergence_diff() - float(conv_a[0])) <= 1e-13 * abs(float(conv_a[0]))
     np.testing.assert_allclose(e.W.cpu().numpy(), ref["W"], rtol=1e-13, atol=1e-13)
     e.close()
+
+
+@pytest.mark.parametrize("lanes", ["1", "8"])
+@pytest.mark.parametrize("maxit", ["2", "12"])
+def test_epilogue_partials_with_fallback_chunks(gpu, lanes, maxit):
+    """Path 6 writes the x̄ partials in its epilogue (one chunk per wave, or per block of
+    lane groups); a chunk with a scenario the PDHG fallback solved is recomputed from x by
+    the consumer.  PHGPU_IPM_MAXIT sends every scenario (2) or some (12) to the fallback;
+    node_buf (phgpu_ph_reduce), the folded one-rank step (phgpu_ph_step_local) and conv must
+    equal the sums of phbase.py:54-79 / 330-339 over the engine's own x."""
+    import os
+    from mpisppy_amd import _lib
+    keep = {k: os.environ.get(k) for k in ("PHGPU_IPM_MAXIT", "PHGPU_IPM_LANES")}
+    os.environ["PHGPU_IPM_LANES"] = lanes
+    try:
+        e = _engine("farmer", 1000)
+        e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
+        e.compute_xbar()                        # finds out the wave / node layout (once)
+        e.set_rho(1.0)
+        e.set_terms(1, 1)
+        e.update(True)
+        e.convergence_diff()
+        os.environ["PHGPU_IPM_MAXIT"] = maxit
+        e.solve(_lib.default_options(), warm=True)
+        assert e.kernel_info()["path"] == 6 and int(e.ipm_info()["lanes"]) == int(lanes)
+        it = e.host("iters")
+        assert (e.host("status") == 0).all()
+        fell = int((it > int(maxit)).sum())
+        assert fell > 0 and (maxit != "2" or fell == e.S), fell
+        e.node_buf.fill_(1e30)
+        e.compute_xbar()
+        ref = _expected_node_buf(e)
+        np.testing.assert_allclose(e.node_buf.cpu().numpy(), ref, rtol=1e-13, atol=1e-12)
+        # the folded step of one rank, from the same partials
+        x = e.x.cpu().numpy()[e.batch_ref.nonant_col]
+        half = e.num_nodes * e.nlen_max
+        xb = ref[:half][:e.nn]
+        conv_ref = np.abs(x - xb[:, None]).sum() / (e.S * e.nn)
+        e.node_buf.fill_(1e30)
+        e.compute_xbar(lazy=True)
+        e.update(True)
+        conv = e.convergence_diff()
+        assert abs(conv - conv_ref) <= 1e-12 * max(1.0, conv_ref), (conv, conv_ref)
+        np.testing.assert_allclose(e.host("node_buf"), ref, rtol=1e-13, atol=1e-12)
+        e.close()
+    finally:
+        for k, v in keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
