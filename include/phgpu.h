@@ -234,6 +234,24 @@ int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node_buf, doubl
                         const double* rho, int update_W, double* conv_local, int64_t* stats_out,
                         void* stream);
 
+/* phgpu_ph_step_local, deferred: the step is recorded and runs at the handle's next call.
+ * If that call is a phgpu_solve_deferred that takes path 6 (the batched interior point),
+ * writes other output buffers than x, and the previous solve was path 6 with its x̄
+ * partials for x, the step is folded into the solve launch's prologue:
+ * every block sums the previous solve's partials to x̄, each scenario updates its x̄ / W,
+ * and the grid's last block stores conv_local; stats_out (the previous solve's statistics)
+ * is stored by the same launch.  conv_local and stats_out are written a few microseconds
+ * into the solve: a caller polling them (NaN / -1 sentinels, as phgpu_ph_update_ex
+ * describes) learns the convergence metric while the solve runs.  Any other call on the
+ * handle (or a solve that cannot fold it) first runs the step as phgpu_ph_step_local on
+ * the stream given here.  PHGPU_FUSE_STEP=0 never folds (experiments). */
+int phgpu_ph_step_defer(phgpu_handle h, const double* x, double* node_buf, double* xbar, double* W,
+                        const double* rho, int update_W, double* conv_local, int64_t* stats_out,
+                        void* stream);
+
+/* Run a step deferred by phgpu_ph_step_defer now (no-op if none is pending). */
+int phgpu_ph_step_flush(phgpu_handle h);
+
 /* Local probability-weighted sums (spopt.py:310-439) into out[5]:
  *   out[0] = sum_s prob_s * obj_s    out[1] = sum_s prob_s * bound_s
  *   out[2] = sum_s prob_s (E1)       out[3] = sum_{s feasible} prob_s, where feasible
@@ -287,14 +305,15 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
-/* Path-6 (interior point) diagnostics: info[11] = {1 if path 6 applies to the pattern,
+/* Path-6 (interior point) diagnostics: info[12] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
  * and 2 if the module failed to compile or load (path 6 is then not the automatic path
  * until new data arrives by phgpu_set_scenarios), 1 if a module is compiled, rows in its normal
  * equations, its factor entries, its scratch bytes per lane, its hipRTC compile seconds,
  * flops of one LDL' factorisation, flops of one forward + backward solve, lanes per
  * scenario of its IPM kernel (1, or a lane group of 2..16: more lanes for fewer local
- * scenarios, PHGPU_IPM_LANES pins it)}. */
+ * scenarios, PHGPU_IPM_LANES pins it), PH steps folded into solve launches so far
+ * (phgpu_ph_step_defer)}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
 /* The path-6 source the library generates for a pattern and its data flags (host code

@@ -177,6 +177,22 @@ struct phgpu_state {
     // the update kernels' last-block reduction of conv: per-block partials and a counter
     double* cpart_blk;
     int32_t* blk_cnt;
+    // a one-rank PH step deferred by phgpu_ph_step_defer: folded into the next path-6
+    // deferred solve's prologue (jit_ph_step.hip.in) when it can be, else run by
+    // phgpu_ph_step_local before that solve or before any other call
+    struct ph_pending {
+        int active = 0;
+        const double* x = nullptr;
+        double *node_buf = nullptr, *xbar = nullptr, *W = nullptr;
+        const double* rho = nullptr;
+        int update_W = 0;
+        double* conv = nullptr;
+        int64_t* stats = nullptr;
+        hipStream_t stream = nullptr;
+    } pend;
+    int fuse_now;      // ipm_launch folds pend into this launch
+    int64_t folded;    // PH steps folded into solve launches so far (phgpu_ipm_info)
+    int32_t* nb_idx;   // [nn] node_buf index (node of the local scenarios, offset) of nonant k (two-stage)
 };
 
 #define IX(k) ((size_t)(k) * (size_t)S + (size_t)s)
@@ -1695,6 +1711,24 @@ static int build_sell(phgpu_state* h, const int32_t* row_ptr, const int32_t* col
                     &h->cw_ptr, &h->cw_slc);
 }
 
+static int step_local_impl(phgpu_state* h, const double* x, double* node_buf, double* xbar, double* W,
+                           const double* rho, int update_W, double* conv_local, int64_t* stats_out, hipStream_t st);
+
+static bool xp_valid(const phgpu_state* h, const double* x);
+
+// run a deferred PH step now (its recorded stream), if one is pending
+static int flush_step(phgpu_state* h) {
+    if (!h || !h->pend.active) return 0;
+    phgpu_state::ph_pending q = h->pend;
+    h->pend.active = 0;
+    return step_local_impl(h, q.x, q.node_buf, q.xbar, q.W, q.rho, q.update_W, q.conv, q.stats, q.stream);
+}
+#define FLUSH_STEP(h)                      \
+    do {                                   \
+        const int frc_ = flush_step(h);    \
+        if (frc_) return frc_;             \
+    } while (0)
+
 extern "C" int phgpu_default_options(phgpu_options* o) {
     if (!o) return set_err(-1, "null options");
     o->eps_rel = 1e-9;
@@ -1921,7 +1955,7 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
                 ALLOC(h->xp_dirty[k], nch);
             }
         }
-        ALLOC(h->cpart_blk, (Sz + BLOCK - 1) / BLOCK + 1);
+        ALLOC(h->cpart_blk, (Sz + 15) / 16 + 1);  // one per block of the widest grid (path-6 lane groups of 16)
         ALLOC(h->blk_cnt, 4);
         if (hipMemset(h->blk_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess) {
             phgpu_destroy(h);
@@ -2106,6 +2140,8 @@ static int set_scenarios_shared(phgpu_state* h, const double* A_val, const doubl
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     h->xbar_mixed = -1;
+    if (h->nb_idx) (void)hipFree(h->nb_idx);
+    h->nb_idx = nullptr;
     const int big = std::max(nnz, std::max(n, m));
     const dim3 gb((unsigned)((big + 255) / 256)), gn((unsigned)((n + 255) / 256)), gm((unsigned)((m + 255) / 256));
     const dim3 gz((unsigned)((nnz + 255) / 256 > 0 ? (nnz + 255) / 256 : 1));
@@ -2217,6 +2253,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
                                    const double* ru, const double* q, const double* obj_const,
                                    const double* prob, const int32_t* node_of,
                                    const double* prob_coeff, void* stream) {
+    FLUSH_STEP(h);
     if (!h) return set_err(-1, "null handle");
     if ((h->nnz && !A_val) || !c || !lb || !ub || (h->m && (!rl || !ru)) || !prob || !node_of || !prob_coeff)
         return set_err(-1, "null scenario array");
@@ -2241,6 +2278,8 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     HIPCHK(cp(h->pcoef, prob_coeff, (size_t)h->depth * Sz));
     HIPCHK(hipMemcpyAsync(h->node_of, node_of, (size_t)h->depth * Sz * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     h->xbar_mixed = -1;
+    if (h->nb_idx) (void)hipFree(h->nb_idx);
+    h->nb_idx = nullptr;
     h->wslot = h->wq = 0;
     h->pending = -1;
     h->have_s[0] = h->have_s[1] = 0;
@@ -2263,6 +2302,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
 
 extern "C" int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
                                   const double* xbar, int W_on, int prox_on) {
+    FLUSH_STEP(h);
     if (!h) return set_err(-1, "null handle");
     if (h->nn > 0 && ((W_on && !W) || (prox_on && (!rho || !xbar))))
         return set_err(-1, "W / rho / xbar pointer missing for the requested terms");
@@ -2428,6 +2468,23 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             h->ipm_off = 1;  // the automatic choice falls back to the handle's PDHG path
             path = default_path(h);
         }
+    }
+    // a deferred one-rank PH step (phgpu_ph_step_defer): folded into this launch's prologue
+    // when it is a path-6 deferred solve that writes other buffers than the step reads and
+    // the previous solve's partials / statistics are path 6's; else run now
+    h->fuse_now = 0;
+    if (h->pend.active) {
+        const phgpu_state::ph_pending& q = h->pend;
+        const char* fe = getenv("PHGPU_FUSE_STEP");
+        const bool fuse = path == 6 && defer && !(fe && atoi(fe) == 0) && q.stream == st && q.x != x &&
+                          h->nb_idx && h->xbar_single && h->xbar_mixed == 0 && h->nn > 0 && h->nn <= XL_NN_MAX &&
+                          xp_valid(h, q.x) && q.W == h->W && q.xbar == h->xbar && q.rho == h->rho &&
+                          (!q.stats || (h->last_stats && h->last_stats == h->ipm_stats + 8 * (1 - h->ipm_parity)));
+        if (fuse) {
+            h->fuse_now = 1;
+            ++h->folded;
+        }
+        else FLUSH_STEP(h);
     }
     const bool use_reg = path == 2;
     int out_rec = 0;  // the warm state this solve writes lives in the records
@@ -2626,6 +2683,7 @@ __global__ void __launch_bounds__(SC_T) k_status_counts(const int32_t* __restric
 
 extern "C" int phgpu_status_counts(phgpu_handle h, const int32_t* status, int32_t* counts, void* stream) {
     if (!h || !status || !counts) return set_err(-1, "null argument");
+    FLUSH_STEP(h);
     hipLaunchKernelGGL(k_status_counts, dim3(1), dim3(SC_T), 0, (hipStream_t)stream, status, h->S, counts);
     HIPCHK(hipGetLastError());
     return 0;
@@ -2658,6 +2716,7 @@ __global__ void __launch_bounds__(SC_T) k_solve_stats(const int32_t* __restrict_
 
 extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
     if (!h || !out) return set_err(-1, "null argument");
+    FLUSH_STEP(h);
     if (!h->last_status) return set_err(-1, "phgpu_solve_stats: no solve yet");
     hipStream_t st = (hipStream_t)stream;
     const unsigned long long* src = h->last_stats;
@@ -2686,6 +2745,21 @@ static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipS
         HIPCHK(hipFree(d));
         h->xbar_mixed = v[0] ? 1 : 0;
         h->xbar_single = v[1] ? 0 : 1;
+        if (h->xbar_single && h->nn > 0 && h->nn <= XL_NN_MAX && !h->nb_idx) {
+            // node_buf index of each nonant (its one node, offset) for the folded PH step
+            std::vector<int32_t> dep(h->nn), off(h->nn), idx(h->nn);
+            HIPCHK(hipMemcpy(dep.data(), h->nonant_depth, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(off.data(), h->nonant_off, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
+            for (int k = 0; k < h->nn; ++k) {
+                int32_t g = 0;
+                HIPCHK(hipMemcpy(&g, h->node_of + (size_t)dep[k] * h->S, sizeof(int32_t), hipMemcpyDeviceToHost));
+                idx[k] = g * h->nlen_max + off[k];
+            }
+            int32_t* di = nullptr;
+            HIPCHK(hipMalloc((void**)&di, h->nn * sizeof(int32_t)));
+            HIPCHK(hipMemcpy(di, idx.data(), h->nn * sizeof(int32_t), hipMemcpyHostToDevice));
+            h->nb_idx = di;
+        }
     }
     if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
     hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
@@ -2709,6 +2783,7 @@ static phgpu_state xp_view(const phgpu_state* h) {  // the state with part = the
 
 extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
     if (!h || !x || !node_buf) return set_err(-1, "null argument");
+    FLUSH_STEP(h);
     hipStream_t st = (hipStream_t)stream;
     const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
     if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
@@ -2752,6 +2827,7 @@ extern "C" int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double*
     if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
         return set_err(-1, "null argument");
     if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_update_ex: stats_out before any solve");
+    FLUSH_STEP(h);
     hipStream_t st = (hipStream_t)stream;
     conv_sink o;
     const int rc = make_sink(h, conv_local, stats_out, st, o);
@@ -2775,7 +2851,39 @@ extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node
     if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
         return set_err(-1, "null argument");
     if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_step_local: stats_out before any solve");
-    hipStream_t st = (hipStream_t)stream;
+    FLUSH_STEP(h);
+    return step_local_impl(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, (hipStream_t)stream);
+}
+
+extern "C" int phgpu_ph_step_defer(phgpu_handle h, const double* x, double* node_buf, double* xbar, double* W,
+                                   const double* rho, int update_W, double* conv_local, int64_t* stats_out,
+                                   void* stream) {
+    if (!h || !x || !node_buf || !xbar || !conv_local || (update_W && (!W || !rho)))
+        return set_err(-1, "null argument");
+    if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_step_defer: stats_out before any solve");
+    FLUSH_STEP(h);
+    phgpu_state::ph_pending& q = h->pend;
+    q.active = 1;
+    q.x = x;
+    q.node_buf = node_buf;
+    q.xbar = xbar;
+    q.W = W;
+    q.rho = rho;
+    q.update_W = update_W ? 1 : 0;
+    q.conv = conv_local;
+    q.stats = stats_out;
+    q.stream = (hipStream_t)stream;
+    return 0;
+}
+
+extern "C" int phgpu_ph_step_flush(phgpu_handle h) {
+    if (!h) return set_err(-1, "null handle");
+    return flush_step(h);
+}
+
+static int step_local_impl(phgpu_state* h, const double* x, double* node_buf, double* xbar, double* W,
+                           const double* rho, int update_W, double* conv_local, int64_t* stats_out, hipStream_t st) {
+    void* stream = (void*)st;
     if (h->nn == 0 || h->nn > XL_NN_MAX || h->xbar_mixed != 0 || !h->xbar_single) {
         // the general route (also the first call, which finds out xbar_mixed / _single)
         const int rc = phgpu_ph_reduce(h, x, node_buf, stream);
@@ -2806,6 +2914,7 @@ extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node
 extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const double* bound,
                                   const int32_t* status, double* out, void* stream) {
     if (!h || !obj || !bound || !status || !out) return set_err(-1, "null argument");
+    FLUSH_STEP(h);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_expect_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, obj, bound, status);
     HIPCHK(hipGetLastError());
@@ -2817,6 +2926,7 @@ extern "C" int phgpu_expectations(phgpu_handle h, const double* obj, const doubl
 
 extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* stream) {
     if (!h) return set_err(-1, "null handle");
+    FLUSH_STEP(h);
     if (h->nn == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (h->shared) {
@@ -2836,6 +2946,7 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
 
 extern "C" int phgpu_destroy(phgpu_handle h) {
     if (!h) return 0;
+    h->pend.active = 0;  // a deferred step that never ran is dropped with the handle
     if (h->oms[0]) {  // the x / y / omega / sk_iters fields may be bound to slot 1: free by slot
         h->x = h->xs[0];
         h->y = h->ys[0];
@@ -2870,7 +2981,7 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
     if (h->stats_gen) (void)hipFree(h->stats_gen);
     {
         void* more[] = {h->xp[0], h->xp[1], h->xp_node[0], h->xp_node[1], h->xp_dirty[0], h->xp_dirty[1],
-                        h->cpart_blk, h->blk_cnt};
+                        h->cpart_blk, h->blk_cnt, h->nb_idx};
         for (void* p : more)
             if (p) (void)hipFree(p);
     }
@@ -2929,8 +3040,9 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     if (!h || !info) return set_err(-1, "null argument");
-    for (int k = 0; k < 11; ++k) info[k] = 0.0;
+    for (int k = 0; k < 12; ++k) info[k] = 0.0;
     info[0] = ipm_eligible(h) ? 1.0 : 0.0;
+    info[11] = (double)h->folded;
     info[1] = h->ipm_nf;
     info[2] = h->ipm_off;
     if (h->ipm) {

@@ -48,7 +48,7 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_expectations",
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats",
-           "phgpu_ph_update_ex", "phgpu_ph_step_local"]
+           "phgpu_ph_update_ex", "phgpu_ph_step_local", "phgpu_ph_step_defer", "phgpu_ph_step_flush"]
 
 _lib = None
 
@@ -81,6 +81,8 @@ def load(path=None):
     lib.phgpu_ph_update.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]
     lib.phgpu_ph_update_ex.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]
     lib.phgpu_ph_step_local.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]
+    lib.phgpu_ph_step_defer.argtypes = lib.phgpu_ph_step_local.argtypes
+    lib.phgpu_ph_step_flush.argtypes = [c_vp]
     lib.phgpu_expectations.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]
     lib.phgpu_fix_nonants.argtypes = [c_vp, c_vp, c_vp]
     lib.phgpu_status_counts.argtypes = [c_vp, c_vp, c_vp, c_vp]

@@ -167,6 +167,7 @@ class PHEngine:
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
+            self._flush_step()
             torch.cuda.synchronize(self.device)
             self.lib.phgpu_destroy(self.h)
             self.h = None
@@ -190,16 +191,17 @@ class PHEngine:
 
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
-        info = (ctypes.c_double * 11)()
+        info = (ctypes.c_double * 12)()
         _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
         keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
-                "factor_flops", "solve_flops", "lanes"]
+                "factor_flops", "solve_flops", "lanes", "folded_steps"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):
         """rho: scalar, host [nn] array (the same per-nonant rho in every scenario) or host
         [S, nn] array (the rho Params of phbase.py:598-602)."""
+        self._flush_step()
         if np.isscalar(rho):
             self.rho.fill_(float(rho))
         elif np.ndim(rho) == 1:
@@ -210,9 +212,11 @@ class PHEngine:
             self.rho.copy_(_dev_T(np.asarray(rho, dtype=np.float64), self.device))
 
     def set_W(self, W):
+        self._flush_step()
         self.W.copy_(_dev_T(np.asarray(W, dtype=np.float64), self.device))
 
     def set_xbar(self, xbar):
+        self._flush_step()
         self.xbar.copy_(_dev_T(np.asarray(xbar, dtype=np.float64), self.device))
 
     def set_terms(self, W_on, prox_on):
@@ -353,6 +357,7 @@ class PHEngine:
             self._spec_id = self._launch_id
         else:
             self._cur_id = self._launch_id
+        self._step_deferred = False   # the library folds a deferred step into this launch or runs it first
         fn = self.lib.phgpu_solve_deferred if speculative else self.lib.phgpu_solve
         _lib.check(fn(self.h, ctypes.byref(o), 1 if warm else 0, _ptr(out["x"]),
                       _ptr(out["y"] if self.want_duals else None), _ptr(out["obj"]), _ptr(out["bound"]),
@@ -422,15 +427,24 @@ class PHEngine:
         return self.node_buf
 
     def _flush_xbar(self):
+        self._flush_step()
         if getattr(self, "_xbar_pending", False):
             self.compute_xbar()
 
-    def update(self, update_W=True):
+    def _flush_step(self):
+        """Run a step phgpu_ph_step_defer still holds (no solve has folded it yet)."""
+        if getattr(self, "_step_deferred", False):
+            self._step_deferred = False
+            _lib.check(self.lib.phgpu_ph_step_flush(self.h), "phgpu_ph_step_flush")
+
+    def update(self, update_W=True, defer=False):
         """Scatter x̄, W += rho (x - x̄), local conv (phbase.py:90-103, 293-339).  One rank:
         conv goes straight to pinned host memory (no copy launch; with several ranks it
         stays on the device for the all-reduce).  The last launch's statistics go to
         pinned host memory in the same kernel (the gripe and the instrumentation read
-        them there)."""
+        them there).  ``defer`` (one rank, x̄ pending: PHBase.iterk_loop's speculative
+        step) hands the step to phgpu_ph_step_defer, which folds it into the next solve
+        launch when it can; the solve must follow before anything reads W."""
         self._conv_zero_copy = self.comm.size == 1
         conv = self._conv_host if self._conv_zero_copy else self.conv_buf
         self._conv_np[0] = float("nan")     # the readback's sentinel (before the launch)
@@ -452,9 +466,11 @@ class PHEngine:
         self._wait_stats = stats.numpy() if (stats is not None and self._conv_zero_copy) else None
         if getattr(self, "_xbar_pending", False):
             self._xbar_pending = False
-            _lib.check(self.lib.phgpu_ph_step_local(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
-                                                    _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
-                                                    _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_step_local")
+            fn = self.lib.phgpu_ph_step_defer if defer else self.lib.phgpu_ph_step_local
+            _lib.check(fn(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
+                          _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
+                          _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_step")
+            self._step_deferred = bool(defer)
             return
         _lib.check(self.lib.phgpu_ph_update_ex(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
                                                _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
@@ -490,6 +506,7 @@ class PHEngine:
     def convergence_wait(self):
         """The pending conv (polls the pinned word; after a long wait it synchronises the
         streams, which also surfaces a device error)."""
+        self._flush_step()          # a deferred step no solve has taken yet: run it now
         a = self._conv_np
         st = self._wait_stats if self._conv_zero_copy else None
         n = 0
@@ -546,6 +563,7 @@ class PHEngine:
         return self.x.index_select(0, idx).T.cpu().numpy()
 
     def host(self, name):
+        self._flush_step()
         if name == "node_buf":
             self._flush_xbar()
         t = getattr(self, name)

@@ -119,9 +119,10 @@ class PHBase(SPOpt):
         # with one rank the engine folds x̄ into the Update_W launch (engine.compute_xbar)
         self.engine.compute_xbar(lazy=True)
 
-    # phbase.py:293-318 (fused with the x̄ scatter and the conv partial sum)
+    # phbase.py:293-318 (fused with the x̄ scatter and the conv partial sum; in the
+    # speculative loop deferred into the next solve launch, engine.update(defer=True))
     def Update_W(self, verbose=False):
-        self.engine.update(update_W=True)
+        self.engine.update(update_W=True, defer=getattr(self, "_defer_update", False))
 
     # phbase.py:321-343
     def convergence_diff(self):
@@ -259,14 +260,19 @@ class PHBase(SPOpt):
             t0 = time.perf_counter()
             if dprogress:
                 global_toc(f"\nInitiating PH Iteration {self._PHIter}\n", self.cylinder_rank == 0)
-            self.Compute_Xbar(verbose)
-            self.Update_W(verbose)
             # Speculative solve: the next solve_loop only depends on W and x̄, which are
             # final here, so it is launched before the convergence readback and committed
             # after the test (discarded when the loop stops) -- the GPU does not idle
             # while the host reads conv and returns to launch the solve.  Off when an
-            # extension could change the problem between the test and the solve.
+            # extension could change the problem between the test and the solve.  With it,
+            # one rank's x̄ / W / conv step runs in the solve launch itself.
             spec = self._speculate(have_ext)
+            self.Compute_Xbar(verbose)
+            self._defer_update = spec
+            try:
+                self.Update_W(verbose)
+            finally:
+                self._defer_update = False
             if spec:
                 self.engine.convergence_diff_async()
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,

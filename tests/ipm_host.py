@@ -37,6 +37,15 @@ template <class T> static inline T __shfl_xor(T, int, int) { return T(0); }  // 
 template <class T> static inline T __shfl_down(T, int, int) { return T(0); }
 template <class T> static inline T __shfl(T v, int, int) { return v; }
 static inline bool __any(bool b) { return b; }
+#define __shared__ static
+static inline void __syncthreads() {}
+static ipm_dim3 gridDim;
+#define __HIP_MEMORY_SCOPE_AGENT 0
+#define __HIP_MEMORY_SCOPE_SYSTEM 0
+template <class T> static inline T __hip_atomic_exchange(T* p, T v, int, int) { T o = *p; *p = v; return o; }
+template <class T> static inline T __hip_atomic_fetch_add(T* p, T v, int, int) { T o = *p; *p += v; return o; }
+template <class T> static inline void __hip_atomic_store(T* p, T v, int, int) { *p = v; }
+#define PHS_ORDER(v) (void)(v)
 """
 
 DRIVER = r"""
@@ -83,7 +92,13 @@ class _Params(ctypes.Structure):
                    ("eps_rel", ctypes.c_double), ("eps_abs", ctypes.c_double), ("eps_tight", ctypes.c_double),
                    ("max_ipm", ctypes.c_int), ("x_in", _VP), ("y_in", _VP), ("stats", _VP), ("stats_zero", _VP),
                    # x̄ partials of the epilogue (null here: the host run skips them)
-                   ("xp", _VP), ("xp_node", _VP), ("xp_dirty", _VP), ("pcoef", _VP), ("node_of", _VP)])
+                   ("xp", _VP), ("xp_node", _VP), ("xp_dirty", _VP), ("pcoef", _VP), ("node_of", _VP),
+                   # the folded PH step (jit_ph_step.hip.in ph_step; on = 0 here)
+                   ("ph_on", ctypes.c_int), ("ph_update_W", ctypes.c_int)]
+                + [(f"ph_{f}", _VP) for f in ("xprev", "xp", "xp_dirty")] + [("ph_xp_n", ctypes.c_longlong),
+                   ("ph_C", ctypes.c_int)] + [(f"ph_{f}", _VP) for f in ("node_buf", "nb_idx")]
+                + [("ph_nb_half", ctypes.c_longlong)] + [(f"ph_{f}", _VP) for f in ("W", "xbar", "rho", "conv", "stats_dst")]
+                + [("ph_scale", ctypes.c_double), ("ph_cpart", _VP), ("ph_cnt", _VP)])
 
 
 def solve(batch, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13,

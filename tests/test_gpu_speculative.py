@@ -8,7 +8,13 @@ library's second slot, made current only by phgpu_commit.  So a run with the spe
 solve and one without give bit-identical x̄, W, conv and iteration counts, and a solve
 after the convergence break warm-starts from the last committed iterate in both --
 checked here bit for bit on the register path in scenario order and in record mode, on
-the global-memory kernel, and on the multistage aircond tree.
+the global-memory kernel, and on the multistage aircond tree (with the one-rank step run as
+its own launch, PHGPU_FUSE_STEP=0).
+
+With one rank, path 6 and a two-stage tree the speculative loop also folds the x̄ / W /
+conv step into the solve launch (phgpu_ph_step_defer): its sums run in
+another grid partition, so that run is checked against the unfolded one to 1e-12 (x̄, W, x)
+and for the same PH iteration count.
 """
 import os
 
@@ -74,6 +80,8 @@ CASES = {
 def test_speculative_solve_is_invisible(gpu, case):
     keep = os.environ.get("PHGPU_REG_REC")
     keep_ipm = os.environ.get("PHGPU_IPM")
+    keep_fuse = os.environ.get("PHGPU_FUSE_STEP")
+    os.environ["PHGPU_FUSE_STEP"] = "0"
     if case == "farmer4096_record_mode":
         os.environ["PHGPU_REG_REC"] = "1"
         os.environ["PHGPU_IPM"] = "0"
@@ -81,7 +89,7 @@ def test_speculative_solve_is_invisible(gpu, case):
         a = _run(CASES[case], True)
         b = _run(CASES[case], False)
     finally:
-        for k, v in (("PHGPU_REG_REC", keep), ("PHGPU_IPM", keep_ipm)):
+        for k, v in (("PHGPU_REG_REC", keep), ("PHGPU_IPM", keep_ipm), ("PHGPU_FUSE_STEP", keep_fuse)):
             if v is None:
                 os.environ.pop(k, None)
             else:
@@ -93,3 +101,35 @@ def test_speculative_solve_is_invisible(gpu, case):
     assert a["iter"] == b["iter"] and a["conv"] == b["conv"], (a["iter"], b["iter"], a["conv"], b["conv"])
     for k in ("W", "xbar", "node_buf", "x", "x_after", "iters_after"):
         assert np.array_equal(a[k], b[k]), (case, k, np.abs(a[k] - b[k]).max())
+
+
+@pytest.mark.parametrize("S", [4096, 40000])
+def test_folded_step_matches_the_step_launch(gpu, S):
+    """The speculative loop with the PH step folded into the path-6 solve launch (lane
+    groups at 4,096 scenarios, one lane at 40,000) against the same loop with the step as
+    its own launch: the same PH iteration count to conv < 3e-2, x̄ / W / x within 1e-12
+    (the sums run in another grid partition), and the folded path actually taken."""
+    keep = os.environ.get("PHGPU_FUSE_STEP")
+    try:
+        os.environ["PHGPU_FUSE_STEP"] = "0"
+        b = _run(lambda spec: _farmer(S, spec, 3e-2), True)
+        os.environ.pop("PHGPU_FUSE_STEP", None)
+        ph = _farmer(S, True, 3e-2)
+        ph.ph_main(finalize=False)
+        assert ph.converged
+        e = ph.engine
+        folded = e.ipm_info()["folded_steps"]
+        a = {"iter": ph._PHIter, "conv": ph.conv, "W": e.W.cpu().numpy().copy(), "xbar": e.xbar.cpu().numpy().copy(),
+             "node_buf": e.node_buf.cpu().numpy().copy(), "x": e.x.cpu().numpy().copy()}
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_FUSE_STEP", None)
+        else:
+            os.environ["PHGPU_FUSE_STEP"] = keep
+    assert e.kernel_info()["path"] == 6
+    assert folded >= a["iter"] - 2, (folded, a["iter"])
+    assert a["iter"] == b["iter"], (a["iter"], b["iter"])
+    assert abs(a["conv"] - b["conv"]) <= 1e-12 * abs(b["conv"]), (a["conv"], b["conv"])
+    for k in ("W", "xbar", "node_buf", "x"):
+        scale = max(1.0, float(np.abs(b[k]).max()))
+        assert np.abs(a[k] - b[k]).max() <= 1e-12 * scale, (k, np.abs(a[k] - b[k]).max())
