@@ -159,6 +159,7 @@ struct phgpu_state {
     // default); the fallback list [S] and its counters {fail_n[2], qhead[2]} by parity
     ipm_module* ipm;
     int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity, ipm_spill1;
+    int ipm_wave;  // WPS of the workgroup IPM for medium scenarios (0: not eligible; jit_ipm_wave.hip.in)
     int32_t *ipm_list, *ipm_cnt;
     // solve statistics (phgpu_solve_stats): path 6 accumulates them in its kernels (by
     // parity, [2][8]); other paths get them from k_solve_stats over the last solve's
@@ -618,10 +619,17 @@ struct solve_params {
 __global__ void __launch_bounds__(BLOCK)
 k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __restrict__ yout,
         double* __restrict__ obj, double* __restrict__ bound, int32_t* __restrict__ status,
-        int32_t* __restrict__ iters) {
+        int32_t* __restrict__ iters, const int32_t* __restrict__ list = nullptr,
+        const int32_t* __restrict__ list_n = nullptr, unsigned long long* __restrict__ stats = nullptr) {
     const int64_t S = st.S;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // list mode (the fallback of path 6's workgroup IPM): lane q solves list[q]
+    if (list) {
+        if (s >= *list_n) return;
+        s = list[s];
+    } else if (s >= S) {
+        return;
+    }
     const int n = st.n, m = st.m;
     const int32_t* __restrict__ row_ptr = st.row_ptr;
     const int32_t* __restrict__ col_idx = st.col_idx;
@@ -891,6 +899,12 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     bound[s] = dobj;
     status[s] = stat;
     if (iters) iters[s] = (stat == PHGPU_ITER_LIMIT) ? P.max_iter : it;
+    if (stats) {  // list mode: this solve's statistics (the IPM counted the others)
+        const unsigned long long its = (unsigned long long)((stat == PHGPU_ITER_LIMIT) ? P.max_iter : it);
+        atomicAdd(&stats[stat], 1ull);
+        atomicAdd(&stats[4], its);
+        atomicMax(&stats[5], its);
+    }
 }
 
 #include "solve_reg.inc"
@@ -1905,7 +1919,9 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     ALLOC(h->stats_gen, 8);
     if (!h->shared) {  // path 6: the pattern's factor size, the fallback list and its counters
         h->ipm_nf = ipm_nf_bound(n, m, row_ptr, col_idx);
-        if (h->ipm_nf > 0) {
+        if (!(h->ipm_nf > 0 && h->ipm_nf <= IPM_MAX_NF && n <= JIT_MAX_N && m <= JIT_MAX_M && nnz <= JIT_MAX_NNZ))
+            h->ipm_wave = ipm_wave_bound(n, m, nnz, row_ptr, col_idx);
+        if (h->ipm_nf > 0 || h->ipm_wave > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 6);
             ALLOC(h->ipm_stats, 16);

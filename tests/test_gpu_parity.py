@@ -92,14 +92,15 @@ def test_farmer30_trivial_bound(gpu):
     assert round(-tb, -3) == 138000.0  # round_pos_sig(137846, 3)
 
 
-@pytest.mark.parametrize("kernel", [0, 2])
+@pytest.mark.parametrize("kernel", [0, 2, 3])
 def test_farmer_cm10_parity(gpu, kernel):
     """Config-2 problem size (cm = 10: n=120, m=61 after presolve) on 16 scenarios vs
     the exact oracle after 5 PH iterations; batch_creator path.  scen3..18: for
     scen0..2 the cm copies of a crop are identical, so their Iter0 LP has a whole
     optimal face and only the objective (trivial bound) is solver-independent.
-    kernel 0 (auto) takes the workgroup-per-scenario path (one wave per scenario, the
-    30-entry acreage row as a long row); kernel 2 the wide-row register instance."""
+    kernel 0 (auto) takes path 6's workgroup interior point (one wave per scenario,
+    jit_ipm_wave.hip.in); kernel 3 the workgroup PDHG (one wave per scenario, the 30-entry
+    acreage row as a long row); kernel 2 the wide-row register instance."""
     from mpisppy_amd.examples import farmer
     g = GOLD["farmer16_cm10_rho1"]
     names = g["names"]
@@ -108,8 +109,12 @@ def test_farmer_cm10_parity(gpu, kernel):
              batch_creator=farmer.batch_creator, iter0_solver_options=so, iterk_solver_options=so)
     conv, eobj, tb = ph.ph_main()
     info = ph.engine.kernel_info()
-    assert info["path"] == 3 and info["wps"] == 1 and (info["wZC"], info["wZR"]) == (3, 4), info
-    assert info["instance"] >= 0 and info["lanes"] == 64 and info["ZR"] >= 30, info
+    if kernel == 0:
+        ii = ph.engine.ipm_info()
+        assert info["path"] == 6 and ii["lanes"] == 64 and ii["scratch_bytes"] == 0, (info, ii)
+    else:
+        assert info["wps"] == 1 and (info["wZC"], info["wZR"]) == (3, 4), info
+        assert info["instance"] >= 0 and info["lanes"] == 64 and info["ZR"] >= 30, info
     assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"])
     assert (ph.engine.host("status") == 0).all()
     assert np.abs(ph.W_array() - np.array(g["W5"])).max() <= ABS

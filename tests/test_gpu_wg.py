@@ -117,12 +117,26 @@ def test_wg_kernel_certifies_infeasibility(gpu, kind, code):
     e.close()
 
 
-def test_farmer_cm64_parity(gpu):
+@pytest.mark.parametrize("wave", ["1", "0"])
+def test_farmer_cm64_parity(gpu, wave):
     """The HBM-scale variant of config 3 (cm = 64: n = 768, m = 385, a 192-entry acreage
     row) at test size: 2048 well-conditioned scenarios (make_golden_scale.py), 5 PH
-    iterations vs the exact oracle."""
+    iterations vs the exact oracle; on path 6's workgroup interior point (the automatic
+    choice, 4 waves per scenario) and on the workgroup PDHG (PHGPU_IPM_WAVE=0)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
+    keep = os.environ.get("PHGPU_IPM_WAVE")
+    os.environ["PHGPU_IPM_WAVE"] = wave
+    try:
+        _cm64_parity(PH, farmer, wave)
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_IPM_WAVE", None)
+        else:
+            os.environ["PHGPU_IPM_WAVE"] = keep
+
+
+def _cm64_parity(PH, farmer, wave):
     g = SCALE["farmer2048_cm64"]
     names = g["names"]
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": -1.0,
@@ -132,8 +146,14 @@ def test_farmer_cm64_parity(gpu):
             scenario_creator_kwargs={"crops_multiplier": 64, "num_scens": len(names)})
     ph.PH_Prep()
     info = ph.engine.kernel_info()
-    assert info["path"] == 3 and info["wps"] >= 2, info
+    if wave == "1":
+        assert info["path"] == 6, info
+    else:
+        assert info["path"] == 3 and info["wps"] >= 2, info
     tb = ph.Iter0()
+    if wave == "1":
+        ii = ph.engine.ipm_info()
+        assert ii["lanes"] == 256 and ii["scratch_bytes"] == 0, ii
     assert (ph.engine.host("status") == 0).all()
     assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"]), (tb, g["trivial_bound"])
     smp = np.array(g["sample"])

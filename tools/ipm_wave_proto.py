@@ -1,0 +1,205 @@
+"""Prototype of path 7's factorisation (TOOL, not product code): the normal equations
+M = A D A' + E of one scenario factored LDL' by one wave of 64 lanes.
+
+The elimination tree (minimum-degree order, solve_ipm.inc ipm_analyse) is cut below a
+small top set R (<= RMAX rows, upward closed): the rest falls into independent subtrees
+("components"), which are packed onto lanes longest-first.  A lane eliminates its
+components alone (the factor's non-root entries live in the wave's LDS, each written by
+one lane only) and accumulates its Schur updates of the R x R block, which one wave sum
+completes; every lane then factors that dense block itself.  The triangular solves follow
+the same split.  Farmer cm = 10: R = 3 rows, 29 two-row components; cm = 64: 191.
+
+This file builds the tables exactly as the generator does and runs the lanes one after
+another in numpy, so the algorithm and the tables are checked on the CPU against a dense
+solve (python tools/ipm_wave_proto.py).
+"""
+import sys
+
+import numpy as np
+
+
+def analyse(n, m, rp, ci, active):
+    """Minimum-degree order and LDL' pattern (ipm_analyse): order, rank, lcol."""
+    colrows = [[] for _ in range(n)]
+    for i in range(m):
+        if active[i]:
+            for k in range(rp[i], rp[i + 1]):
+                colrows[ci[k]].append(i)
+    adj = [set() for _ in range(m)]
+    for j in range(n):
+        for a in colrows[j]:
+            for b in colrows[j]:
+                if a != b:
+                    adj[a].add(b)
+    done = [False] * m
+    order, lcol = [], {}
+    for _ in range(sum(active)):
+        best = -1
+        for i in range(m):
+            if active[i] and not done[i] and (best < 0 or len(adj[i]) < len(adj[best])):
+                best = i
+        done[best] = True
+        order.append(best)
+        nb = sorted(adj[best])
+        for a in nb:
+            adj[a].discard(best)
+            for b in nb:
+                if a != b:
+                    adj[a].add(b)
+        lcol[best] = nb
+        adj[best] = set()
+    rank = {r: t for t, r in enumerate(order)}
+    for r in order:
+        lcol[r].sort(key=lambda u: rank[u])
+    return order, rank, lcol
+
+
+def plan(order, rank, lcol, lanes=64, rmax=8):
+    """Root set, components and the per-lane elimination lists."""
+    parent = {r: (lcol[r][0] if lcol[r] else None) for r in order}
+    kids = {r: [] for r in order}
+    for r in order:
+        if parent[r] is not None:
+            kids[parent[r]].append(r)
+    cost = {}
+    for r in order:  # ascending rank: children first
+        c = len(lcol[r])
+        cost[r] = 1 + c + c * (c + 1) // 2 + sum(cost[k] for k in kids[r])
+    R = [r for r in order if parent[r] is None]
+    comps = [k for r in R for k in kids[r]]
+    while len(R) < rmax and comps:
+        total = sum(cost[c] for c in comps)
+        big = max(comps, key=lambda c: cost[c])
+        if cost[big] > 0.5 * total or (len(kids[big]) >= 2 and len(comps) < lanes):
+            R.append(big)
+            comps.remove(big)
+            comps += kids[big]
+        else:
+            break
+    Rset = set(R)
+    # R is upward closed: every ancestor of an R row is in R
+    for r in R:
+        assert parent[r] is None or parent[r] in Rset
+    R.sort(key=lambda r: rank[r])
+    load = [0] * lanes
+    lane_rows = [[] for _ in range(lanes)]
+    for c in sorted(comps, key=lambda c: -cost[c]):
+        l = int(np.argmin(load))
+        load[l] += cost[c]
+        stack, rows = [c], []
+        while stack:
+            r = stack.pop()
+            rows.append(r)
+            stack += kids[r]
+        lane_rows[l] += rows
+    for l in range(lanes):
+        lane_rows[l].sort(key=lambda r: rank[r])
+    return R, lane_rows, load
+
+
+def factor_and_solve(M, b, order, rank, lcol, R, lane_rows):
+    """The kernel's algorithm on a dense symmetric M (values on the pattern): returns x."""
+    Ridx = {r: t for t, r in enumerate(R)}
+    F = {}  # non-root entries (u, r), r not in R: the lanes' LDS
+    for r in order:
+        if r in Ridx:
+            continue
+        F[(r, r)] = M[r, r]
+        for u in lcol[r]:
+            F[(u, r)] = M[u, r]
+    nR = len(R)
+    # root block: every lane's partial (assembly share + its Schur updates), then one sum
+    part = np.zeros((len(lane_rows), nR, nR))
+    for a in R:
+        for c in R:
+            part[0, Ridx[a], Ridx[c]] = M[a, c]  # (the kernel: column-parallel partials)
+    DI = {}
+    for l, rows in enumerate(lane_rows):
+        for r in rows:
+            d = F[(r, r)]
+            idv = 1.0 / d
+            DI[r] = idv
+            uu = [F[(u, r)] for u in lcol[r]]
+            for iu, u in enumerate(lcol[r]):
+                for iv, v in enumerate(lcol[r]):
+                    if rank[v] > rank[u]:
+                        continue
+                    val = uu[iu] * uu[iv] * idv
+                    if u in Ridx and v in Ridx:
+                        part[l, Ridx[u], Ridx[v]] -= val
+                    else:
+                        assert v not in Ridx and (u, v) in F, (u, v)
+                        F[(u, v)] -= val
+            for iu, u in enumerate(lcol[r]):
+                F[(u, r)] = uu[iu] * idv
+    RB = part.sum(0)
+    # dense LDL' of the root block (lower triangle, rank order)
+    Lr = np.zeros((nR, nR))
+    Dr = np.zeros(nR)
+    A = np.tril(RB)
+    for j in range(nR):
+        Dr[j] = A[j, j] - sum(Lr[j, k] ** 2 * Dr[k] for k in range(j))
+        for i in range(j + 1, nR):
+            Lr[i, j] = (A[i, j] - sum(Lr[i, k] * Lr[j, k] * Dr[k] for k in range(j))) / Dr[j]
+    # forward
+    z = dict(enumerate(b))
+    rpart = np.zeros((len(lane_rows), nR))
+    for l, rows in enumerate(lane_rows):
+        for r in rows:
+            for u in lcol[r]:
+                if u in Ridx:
+                    rpart[l, Ridx[u]] -= F[(u, r)] * z[r]
+                else:
+                    z[u] -= F[(u, r)] * z[r]
+    zr = np.array([b[r] for r in R]) + rpart.sum(0)
+    for i in range(nR):
+        zr[i] -= sum(Lr[i, k] * zr[k] for k in range(i))
+    zr /= Dr
+    for i in reversed(range(nR)):
+        zr[i] -= sum(Lr[k, i] * zr[k] for k in range(i + 1, nR))
+    x = {}
+    for t, r in enumerate(R):
+        x[r] = zr[t]
+    for r in order:
+        if r not in Ridx:
+            z[r] *= DI[r]
+    for l, rows in enumerate(lane_rows):
+        for r in reversed(rows):
+            v = z[r]
+            for u in lcol[r]:
+                v -= F[(u, r)] * x[u]
+            x[r] = v
+    return np.array([x.get(i, 0.0) for i in range(len(b))])
+
+
+def main():
+    sys.path.insert(0, "mpi-sppy-1_amd")
+    from mpisppy_amd.examples import farmer
+    rng = np.random.default_rng(0)
+    for cm in (1, 10, 64):
+        b = farmer.batch_creator(farmer.scenario_names_creator(4), crops_multiplier=cm, num_scens=4)
+        n, m = b.n, b.m
+        active = [bool(np.isfinite(b.rl[0][i]) or np.isfinite(b.ru[0][i])) for i in range(m)]
+        order, rank, lcol = analyse(n, m, b.row_ptr, b.col_idx, active)
+        R, lane_rows, load = plan(order, rank, lcol)
+        A = b.dense_A(0)[[r for r in range(m)]]
+        D = rng.uniform(0.1, 10.0, n)
+        E = rng.uniform(0.01, 1.0, m)
+        M = (A * D) @ A.T + np.diag(E)
+        act = np.array(active)
+        M[~act, :] = 0.0
+        M[:, ~act] = 0.0
+        M[~act, ~act] = 1.0
+        rhs = rng.normal(size=m)
+        rhs[~act] = 0.0
+        x = factor_and_solve(M, rhs, order, rank, lcol, R, lane_rows)
+        ref = np.linalg.solve(M, rhs)
+        err = np.abs(x - ref)[act].max() / np.abs(ref).max()
+        busy = sum(1 for rows in lane_rows if rows)
+        print(f"cm={cm}: rows {len(order)}, root {len(R)}, lanes busy {busy}, max/mean lane load "
+              f"{max(load)}/{np.mean([v for v in load if v]):.1f}, rel err {err:.2e}")
+        assert err < 1e-10
+
+
+if __name__ == "__main__":
+    main()
