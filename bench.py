@@ -265,7 +265,8 @@ def roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir):
     units = float(np.mean([u for _, u in launches]))
     F = ipm_flops_per_iter(b, ipm)
     tflops = F * units / (launch_ms * 1e-3) / 1e12
-    kname = "k_solve_ipm" if int(ipm.get("lanes", 1)) <= 1 else "k_solve_ipm_ml"
+    lanes = int(ipm.get("lanes", 1))
+    kname = "k_solve_ipm" if lanes <= 1 else ("k_solve_ipm_ml" if lanes < 64 else "k_solve_ipm_wave")
     traffic, src = None, None
     pmc = _latest_profile_file(f"pmc_summary_{tag}.json", pdir)
     if pmc:
