@@ -266,7 +266,8 @@ def roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir):
     F = ipm_flops_per_iter(b, ipm)
     tflops = F * units / (launch_ms * 1e-3) / 1e12
     lanes = int(ipm.get("lanes", 1))
-    kname = "k_solve_ipm" if lanes <= 1 else ("k_solve_ipm_ml" if lanes < 64 else "k_solve_ipm_wave")
+    kname = {1: "k_solve_ipm", 2: "k_solve_ipm_ml", 3: "k_solve_ipm_wave", 4: "k_solve_ipm_blk"}.get(
+        int(ipm.get("kernel", 0)), "k_solve_ipm" if lanes <= 1 else ("k_solve_ipm_ml" if lanes < 64 else "k_solve_ipm_wave"))
     traffic, src = None, None
     pmc = _latest_profile_file(f"pmc_summary_{tag}.json", pdir)
     if pmc:

@@ -159,7 +159,8 @@ struct phgpu_state {
     // default); the fallback list [S] and its counters {fail_n[2], qhead[2]} by parity
     ipm_module* ipm;
     int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity, ipm_spill1;
-    int ipm_wave;  // WPS of the workgroup IPM for medium scenarios (0: not eligible; jit_ipm_wave.hip.in)
+    int ipm_wave;  // waves per scenario of the workgroup IPMs for medium scenarios (0: not eligible;
+                   // jit_ipm_blk.hip.in for block-angular patterns, else jit_ipm_wave.hip.in)
     int32_t *ipm_list, *ipm_cnt;
     // solve statistics (phgpu_solve_stats): path 6 accumulates them in its kernels (by
     // parity, [2][8]); other paths get them from k_solve_stats over the last solve's
@@ -1920,7 +1921,7 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
     if (!h->shared) {  // path 6: the pattern's factor size, the fallback list and its counters
         h->ipm_nf = ipm_nf_bound(n, m, row_ptr, col_idx);
         if (!(h->ipm_nf > 0 && h->ipm_nf <= IPM_MAX_NF && n <= JIT_MAX_N && m <= JIT_MAX_M && nnz <= JIT_MAX_NNZ))
-            h->ipm_wave = ipm_wave_bound(n, m, nnz, row_ptr, col_idx);
+            h->ipm_wave = ipm_wg_bound(n, m, nnz, row_ptr, col_idx);
         if (h->ipm_nf > 0 || h->ipm_wave > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 6);
@@ -2495,12 +2496,18 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         const bool fuse = path == 6 && defer && !(fe && atoi(fe) == 0) && q.stream == st && q.x != x &&
                           h->nb_idx && h->xbar_single && h->xbar_mixed == 0 && h->nn > 0 && h->nn <= XL_NN_MAX &&
                           xp_valid(h, q.x) && q.W == h->W && q.xbar == h->xbar && q.rho == h->rho &&
-                          (!q.stats || (h->last_stats && h->last_stats == h->ipm_stats + 8 * (1 - h->ipm_parity)));
+                          (!q.stats || (stats_keep && stats_keep == h->ipm_stats + 8 * (1 - h->ipm_parity)));
         if (fuse) {
             h->fuse_now = 1;
             ++h->folded;
         }
-        else FLUSH_STEP(h);
+        else {
+            // (the step's statistics are the previous solve's: its in-kernel ones if any)
+            h->last_stats = stats_keep;
+            const int frc = flush_step(h);
+            h->last_stats = nullptr;
+            if (frc) return frc;
+        }
     }
     const bool use_reg = path == 2;
     int out_rec = 0;  // the warm state this solve writes lives in the records
@@ -3056,7 +3063,7 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     if (!h || !info) return set_err(-1, "null argument");
-    for (int k = 0; k < 12; ++k) info[k] = 0.0;
+    for (int k = 0; k < 13; ++k) info[k] = 0.0;
     info[0] = ipm_eligible(h) ? 1.0 : 0.0;
     info[11] = (double)h->folded;
     info[1] = h->ipm_nf;
@@ -3070,6 +3077,7 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
         info[8] = h->ipm->fac_flops;
         info[9] = h->ipm->sol_flops;
         info[10] = h->ipm->L;
+        info[12] = h->ipm->L == 1 ? 1 : (h->ipm->L < 64 ? 2 : (h->ipm->blk ? 4 : 3));
     }
     return 0;
 }

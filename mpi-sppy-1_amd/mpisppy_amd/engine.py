@@ -191,10 +191,10 @@ class PHEngine:
 
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
-        info = (ctypes.c_double * 12)()
+        info = (ctypes.c_double * 13)()
         _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
         keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
-                "factor_flops", "solve_flops", "lanes", "folded_steps"]
+                "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state
@@ -334,7 +334,10 @@ class PHEngine:
         test stops the loop).  An uncommitted speculative solve changes nothing: its
         outputs stay in the spare set and the library keeps its warm-start state in a
         second slot that only phgpu_commit makes current (include/phgpu.h)."""
-        self._flush_xbar()
+        # a pending lazy x̄ is computed now; a deferred PH step stays with the library, which
+        # folds it into this launch or runs it ahead of it (phgpu_ph_step_defer)
+        if getattr(self, "_xbar_pending", False):
+            self.compute_xbar()
         o = options if options is not None else _lib.default_options()
         if speculative:
             if not hasattr(self, "_spec"):

@@ -1,4 +1,5 @@
-"""Run the generated workgroup IPM (jit_ipm_wave.hip.in) on the CPU (TEST INFRASTRUCTURE ONLY).
+"""Run the generated workgroup IPMs (jit_ipm_wave.hip.in, jit_ipm_blk.hip.in) on the CPU (TEST
+INFRASTRUCTURE ONLY).
 
 The library's generator (phgpu_ipm_source, lanes = 64 WPS) emits the text the handle
 compiles with hipRTC; here it is compiled with g++ behind a shim: one std::thread per GPU
@@ -45,6 +46,7 @@ static inline int atomicAdd(int* p, int v) { std::lock_guard<std::mutex> l(g_mu)
 static inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) { std::lock_guard<std::mutex> l(g_mu); unsigned long long o = *p; *p += v; return o; }
 static inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) { std::lock_guard<std::mutex> l(g_mu); unsigned long long o = *p; if (v > o) *p = v; return o; }
 static double g_post[4096];
+template <int NV> static inline void w_bmax(double (&v)[NV], double*);
 template <int NV> static inline void w_bsum(double (&v)[NV], double*) {
     for (int k = 0; k < NV; ++k) {
         g_bar->arrive_and_wait();
@@ -55,6 +57,10 @@ template <int NV> static inline void w_bsum(double (&v)[NV], double*) {
         v[k] = a;
     }
     g_bar->arrive_and_wait();
+}
+template <int NS, int NM> static inline void w_bsum_max(double (&v)[NS], double (&u)[NM], double* r) {
+    w_bsum(v, r);
+    w_bmax(u, r);
 }
 template <int NV> static inline void w_bmax(double (&v)[NV], double*) {
     for (int k = 0; k < NV; ++k) {
@@ -78,7 +84,7 @@ extern "C" void wave_run(ipmw_params* p, long long S) {
         g_bar = &bar;
         std::vector<std::thread> th;
         for (int t = 0; t < WT; ++t)
-            th.emplace_back([p, t]() { threadIdx.x = (unsigned)t; k_solve_ipm_wave(*p); });
+            th.emplace_back([p, t]() { threadIdx.x = (unsigned)t; KNAME(*p); });
         for (auto& x : th) x.join();
     }
 }
@@ -88,7 +94,8 @@ _cache = {}
 
 
 def build(src, workdir="/tmp"):
-    text = SHIM + src + DRIVER
+    kname = "k_solve_ipm_blk" if "k_solve_ipm_blk" in src else "k_solve_ipm_wave"
+    text = SHIM + src + f"#define KNAME {kname}\n" + DRIVER
     key = hashlib.sha1(text.encode()).hexdigest()[:16]
     if key in _cache:
         return _cache[key]

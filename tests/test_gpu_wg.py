@@ -117,26 +117,29 @@ def test_wg_kernel_certifies_infeasibility(gpu, kind, code):
     e.close()
 
 
-@pytest.mark.parametrize("wave", ["1", "0"])
-def test_farmer_cm64_parity(gpu, wave):
+@pytest.mark.parametrize("variant", ["blk", "wave", "pdhg"])
+def test_farmer_cm64_parity(gpu, variant):
     """The HBM-scale variant of config 3 (cm = 64: n = 768, m = 385, a 192-entry acreage
     row) at test size: 2048 well-conditioned scenarios (make_golden_scale.py), 5 PH
-    iterations vs the exact oracle; on path 6's workgroup interior point (the automatic
-    choice, 4 waves per scenario) and on the workgroup PDHG (PHGPU_IPM_WAVE=0)."""
+    iterations vs the exact oracle; on path 6's subtree interior point (the automatic
+    choice: 191 crop subtrees over 192 threads), its workgroup interior point
+    (PHGPU_IPM_BLK=0, 4 waves per scenario) and the workgroup PDHG (PHGPU_IPM_WAVE=0)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
-    keep = os.environ.get("PHGPU_IPM_WAVE")
-    os.environ["PHGPU_IPM_WAVE"] = wave
+    env = {"blk": {}, "wave": {"PHGPU_IPM_BLK": "0"}, "pdhg": {"PHGPU_IPM_WAVE": "0"}}[variant]
+    keep = {k: os.environ.get(k) for k in ("PHGPU_IPM_BLK", "PHGPU_IPM_WAVE")}
+    os.environ.update(env)
     try:
-        _cm64_parity(PH, farmer, wave)
+        _cm64_parity(PH, farmer, variant)
     finally:
-        if keep is None:
-            os.environ.pop("PHGPU_IPM_WAVE", None)
-        else:
-            os.environ["PHGPU_IPM_WAVE"] = keep
+        for k, v in keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
-def _cm64_parity(PH, farmer, wave):
+def _cm64_parity(PH, farmer, variant):
     g = SCALE["farmer2048_cm64"]
     names = g["names"]
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": -1.0,
@@ -146,14 +149,14 @@ def _cm64_parity(PH, farmer, wave):
             scenario_creator_kwargs={"crops_multiplier": 64, "num_scens": len(names)})
     ph.PH_Prep()
     info = ph.engine.kernel_info()
-    if wave == "1":
+    if variant != "pdhg":
         assert info["path"] == 6, info
     else:
         assert info["path"] == 3 and info["wps"] >= 2, info
     tb = ph.Iter0()
-    if wave == "1":
+    if variant != "pdhg":
         ii = ph.engine.ipm_info()
-        assert ii["lanes"] == 256 and ii["scratch_bytes"] == 0, ii
+        assert ii["lanes"] == (192 if variant == "blk" else 256) and ii["scratch_bytes"] == 0, ii
     assert (ph.engine.host("status") == 0).all()
     assert abs(tb - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"]), (tb, g["trivial_bound"])
     smp = np.array(g["sample"])
