@@ -24,21 +24,24 @@ from test_gpu_parity import OBJ_REL
 pytestmark = pytest.mark.gpu
 
 
-def arrow_batch(S, blocks, seed, with_q=False, link=2, bad=None):
+def arrow_batch(S, blocks, seed, with_q=False, link=2, bad=None, shapes="random"):
     """S scenarios sharing a block-arrow pattern: per block 3 columns and 2 rows (random
-    entries), plus ``link`` rows each over every third column (long rows when blocks > 12),
-    like farmer's crops and acreage row.  Feasible and bounded by construction; scenario
-    ``bad`` (if given) gets every column bounded by 10 and a first-block row that needs
-    1e6: primal infeasible."""
+    entries; ``shapes`` "full": every block dense, one shape; "two": odd blocks lack one
+    entry, two shapes), plus ``link`` rows each over every third column (long rows when
+    blocks > 12), like farmer's crops and acreage row.  Feasible and bounded by
+    construction; scenario ``bad`` (if given) gets every column bounded by 10 and a
+    first-block row that needs 1e6: primal infeasible."""
     from mpisppy_amd.batch import ScenarioBatch
     rng = np.random.default_rng(seed)
     n, m = 3 * blocks, 2 * blocks + link
     mask = np.zeros((m, n), bool)
     for bk in range(blocks):
         for r in (2 * bk, 2 * bk + 1):
-            mask[r, 3 * bk:3 * bk + 3] = rng.random(3) < 0.8
+            mask[r, 3 * bk:3 * bk + 3] = rng.random(3) < 0.8 if shapes == "random" else True
             if not mask[r].any():
                 mask[r, 3 * bk + rng.integers(3)] = True
+        if shapes == "two" and bk % 2:
+            mask[2 * bk, 3 * bk + 2] = False
     for l in range(link):
         mask[2 * blocks + l, l::3] = True
     rows, cols = np.nonzero(mask)
