@@ -518,9 +518,12 @@ def main():
                 scenario_creator_kwargs={"branching_factors": a.bf, **AIRCOND_KW},
                 all_nodenames=create_nodenames_from_branching_factors(a.bf))
         workload = f"aircond multistage PH (config 4), bf {'x'.join(map(str, a.bf))}"
+    log(f"[bench] model built ({time.perf_counter() - t_setup:.1f} s)")
     with contextlib.redirect_stdout(sys.stderr):
         ph.PH_Prep()
+        log(f"[bench] PH_Prep done ({time.perf_counter() - t_setup:.1f} s)")
         trivial_bound = ph.Iter0()
+        log(f"[bench] Iter0 done ({time.perf_counter() - t_setup:.1f} s)")
         e = ph.engine
         b = ph.batch
         # Iter0's certification, summed over ranks: scenarios whose LP / QP stopped at the
@@ -536,6 +539,7 @@ def main():
         tag = {"farmer": f"farmer{b.S}_cm{a.cm}", "uc": f"uc{b.S}", "aircond": f"aircond{b.S}"}[a.model]
         ph.iterk_loop()                                # W warmup iterations (untimed)
         torch.cuda.synchronize()
+        log(f"[bench] warmup done ({time.perf_counter() - t_setup:.1f} s)")
         t_setup = time.perf_counter() - t_setup
         # HIP events around one solve launch in INSTRUMENT_EVERY (each event is a marker
         # packet that idles the GPU ~5.6 us; the other steps run exactly as the product loop)

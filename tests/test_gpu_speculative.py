@@ -107,8 +107,10 @@ def test_speculative_solve_is_invisible(gpu, case):
 def test_folded_step_matches_the_step_launch(gpu, S):
     """The speculative loop with the PH step folded into the path-6 solve launch (lane
     groups at 4,096 scenarios, one lane at 40,000) against the same loop with the step as
-    its own launch: the same PH iteration count to conv < 3e-2, x̄ / W / x within 1e-12
-    (the sums run in another grid partition), and the folded path actually taken."""
+    its own launch: the same PH iteration count to conv < 3e-2, the folded path actually
+    taken, and x̄ / W / x / conv within 1e-8 relative: the x̄ sums run in another grid
+    partition (bits differ at 1e-16), and over a hundred PH iterations the interior point's
+    own stopping points amplify that to ~1e-10 (40,000 scenarios: conv 3e-10 relative)."""
     keep = os.environ.get("PHGPU_FUSE_STEP")
     try:
         os.environ["PHGPU_FUSE_STEP"] = "0"
@@ -129,7 +131,7 @@ def test_folded_step_matches_the_step_launch(gpu, S):
     assert e.kernel_info()["path"] == 6
     assert folded >= a["iter"] - 2, (folded, a["iter"])
     assert a["iter"] == b["iter"], (a["iter"], b["iter"])
-    assert abs(a["conv"] - b["conv"]) <= 1e-12 * abs(b["conv"]), (a["conv"], b["conv"])
+    assert abs(a["conv"] - b["conv"]) <= 1e-8 * abs(b["conv"]), (a["conv"], b["conv"])
     for k in ("W", "xbar", "node_buf", "x"):
         scale = max(1.0, float(np.abs(b[k]).max()))
-        assert np.abs(a[k] - b[k]).max() <= 1e-12 * scale, (k, np.abs(a[k] - b[k]).max())
+        assert np.abs(a[k] - b[k]).max() <= 1e-8 * scale, (k, np.abs(a[k] - b[k]).max())
