@@ -34,6 +34,7 @@ def main():
             scenario_creator_kwargs={"crops_multiplier": 64, "num_scens": len(names)})
     ph.PH_Prep()
     e = ph.engine
+    e.want_duals = True
     t0 = time.perf_counter()
     ph.Iter0()
     torch.cuda.synchronize()
@@ -46,6 +47,7 @@ def main():
         W = e.host("W")[:, :192].copy()
         xb = e.host("xbar")[:, :192].copy()
         rho = e.host("rho")[:, :192].copy()
+        x_in, y_in = e.host("x").copy(), e.host("y").copy()
         t0 = time.perf_counter()
         ph.solve_loop(solver_options=ph.iterk_solver_options, gripe=False)
         torch.cuda.synchronize()
@@ -58,6 +60,10 @@ def main():
         print(f"PH it {it + 1}: solve {dt * 1e3:.2f} ms, max err {err.max():.3e}, mean err {err.mean():.3e}, "
               f"iters max {its.max()} mean {its.mean():.1f}, status {np.bincount(st, minlength=4)[:4]}, "
               f"x̄ err {np.abs(x.T @ np.full(len(names), 1.0 / len(names)) - xv.mean(0)).max():.3e}", flush=True)
+        dump = os.environ.get("DIAG_DUMP")
+        if dump:  # the worst scenarios' subproblem inputs, for a host-emulation replay
+            np.savez(f"{dump}_it{it + 1}.npz", names=np.array([names[s] for s in worst]), W=W[worst], xbar=xb[worst],
+                     rho=rho[worst], x_in=x_in[worst], y_in=y_in[worst], x=x[worst], xv=xv[worst])
         for s in worst:
             print(f"    scen {names[s]}: err {err[s]:.3e} iters {its[s]} status {st[s]} obj {e.host('obj')[s]:.10g} "
                   f"oracle {ov[s]:.10g}", flush=True)
