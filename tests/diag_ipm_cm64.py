@@ -3,7 +3,7 @@ the automatic path-6 kernel, and every PH subproblem's nonants against the oracl
 proximal solve (oracle/farmer_vec.py prox) with the same W / x̄ / rho.  Prints per PH
 iteration the worst scenarios, their IPM iteration counts and statuses, and the launch time.
 
-    python tests/diag_ipm_cm64.py [iterations] [scenarios]
+    python tests/diag_ipm_cm64.py [iterations] [scenarios] [fixture|first] [crops_multiplier]
 """
 import json
 import os
@@ -27,11 +27,12 @@ def main():
     names = g["names"][:int(sys.argv[2])] if len(sys.argv) > 2 else g["names"]
     if len(sys.argv) > 3 and sys.argv[3] == "first":  # scen0.. (ties at scen0..2, near-ties)
         names = [f"scen{i}" for i in range(len(names))]
+    cm = int(sys.argv[4]) if len(sys.argv) > 4 else 64
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": iters, "defaultPHrho": 1.0, "convthresh": -1.0,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
             "batch_creator": farmer.batch_creator}
     ph = PH(opts, names, farmer.scenario_creator,
-            scenario_creator_kwargs={"crops_multiplier": 64, "num_scens": len(names)})
+            scenario_creator_kwargs={"crops_multiplier": cm, "num_scens": len(names)})
     ph.PH_Prep()
     e = ph.engine
     e.want_duals = True
@@ -39,14 +40,15 @@ def main():
     ph.Iter0()
     torch.cuda.synchronize()
     print("iter0 %.3f s" % (time.perf_counter() - t0), e.kernel_info()["path"], e.ipm_info(), flush=True)
-    bp, sl, f0 = fv.pieces(fv.yields(names, 64), 64)
+    bp, sl, f0 = fv.pieces(fv.yields(names, cm), cm)
     nc = e.batch.nonant_col if hasattr(e, "batch") else ph.batch.nonant_col
     for it in range(iters):
         ph.Compute_Xbar()
         ph.Update_W()
-        W = e.host("W")[:, :192].copy()
-        xb = e.host("xbar")[:, :192].copy()
-        rho = e.host("rho")[:, :192].copy()
+        K = 3 * cm
+        W = e.host("W")[:, :K].copy()
+        xb = e.host("xbar")[:, :K].copy()
+        rho = e.host("rho")[:, :K].copy()
         x_in, y_in = e.host("x").copy(), e.host("y").copy()
         t0 = time.perf_counter()
         ph.solve_loop(solver_options=ph.iterk_solver_options, gripe=False)
@@ -54,7 +56,7 @@ def main():
         dt = time.perf_counter() - t0
         x = e.host("x")[:, nc]
         st, its = e.host("status"), e.host("iters")
-        xv, ov = fv.prox(bp, sl, f0, W, xb, rho, 500.0 * 64)
+        xv, ov = fv.prox(bp, sl, f0, W, xb, rho, 500.0 * cm)
         err = np.abs(x - xv).max(1)
         worst = np.argsort(-err)[:5]
         print(f"PH it {it + 1}: solve {dt * 1e3:.2f} ms, max err {err.max():.3e}, mean err {err.mean():.3e}, "

@@ -1,5 +1,6 @@
-"""Path 6 for medium scenarios: the workgroup interior point (jit_ipm_wave.hip.in,
-DESIGN.md 3.9) -- one workgroup of 64 WPS threads per scenario, the normal equations
+"""Path 6 for medium scenarios: the workgroup interior points -- the subtree kernel
+(jit_ipm_blk.hip.in) for block-angular patterns and the workgroup kernel
+(jit_ipm_wave.hip.in, 3.9) otherwise; one workgroup of 64 WPS threads per scenario, the normal equations
 factored with the elimination tree split into per-thread subtrees and a dense root block
 (tools/ipm_wave_proto.py states the plan and checks it on the CPU).
 
@@ -22,6 +23,19 @@ import pytest
 from test_gpu_parity import OBJ_REL
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _workgroup_ipms_on():
+    """Multi-wave subtree plans and the workgroup kernel are opt-in (PHGPU_IPM_WAVE=1,
+    solve_ipm.inc ipm_wg_bound); these tests check them against the oracle."""
+    keep = os.environ.get("PHGPU_IPM_WAVE")
+    os.environ["PHGPU_IPM_WAVE"] = "1"
+    yield
+    if keep is None:
+        os.environ.pop("PHGPU_IPM_WAVE", None)
+    else:
+        os.environ["PHGPU_IPM_WAVE"] = keep
 
 
 def arrow_batch(S, blocks, seed, with_q=False, link=2, bad=None, shapes="random"):

@@ -16,7 +16,7 @@ step() {
 }
 T="python3 -u -m pytest -m gpu -v --timeout 100 --timeout-method thread"
 step g_par 300 $T tests/test_gpu_scale.py::test_config2_farmer1024_cm10_bound tests/test_gpu_scale.py::test_config2_ph_iterations_to_convergence tests/test_gpu_parity.py::test_farmer_cm10_parity tests/test_gpu_wg.py::test_farmer_cm64_parity tests/test_gpu_ipm_wave.py
-step g_diag 120 python3 -u tests/diag_ipm_cm64.py 4 2048 first
+DIAG_DUMP=gpurun_out/g_worst step g_diag 120 python3 -u tests/diag_ipm_cm64.py 6 2048 first
 B="python3 -u bench.py --no-cpu-baseline"
 step g_cfg2 150 $B --scens 1024 --cm 10
 step g_cm64a 150 $B --cm 64 --scens 2048 --steps 10 --warmup 3
