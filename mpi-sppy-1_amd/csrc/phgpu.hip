@@ -927,9 +927,11 @@ k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict_
     const int half = st.num_nodes * st.nlen_max;
     // no wave spans two nodes (st.xbar_mixed == 0): this kernel does not touch node_buf
     // below, so it clears it for k_xbar_final (one launch less than a memset)
-    if (clear)
+    if (clear && blockIdx.y == 0)
         for (int64_t i = s; i < 2 * (int64_t)half; i += (int64_t)gridDim.x * blockDim.x) node_buf[i] = 0.0;
-    for (int k = 0; k < st.nn; ++k) {
+    // one nonant per grid row (blockIdx.y; see k_ph_update)
+    if ((int)blockIdx.y < st.nn) {
+        const int k = blockIdx.y;
         const int d = st.nonant_depth[k];
         const int gnode = act ? st.node_of[IX(d)] : -1;
         const double w = act ? st.pcoef[IX(d)] : 0.0;
@@ -1133,21 +1135,22 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
     __shared__ double red[XL_T / WAVE];
     __shared__ int last;
     const int wv = threadIdx.x / WAVE, nwb = (int)(blockDim.x / WAVE);
+    const int nblk = (int)(gridDim.x * gridDim.y), bid = (int)(blockIdx.y * gridDim.x + blockIdx.x);
     acc = wave_sum(acc);
     if ((threadIdx.x & (WAVE - 1)) == 0) red[wv] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int u = 0; u < nwb; ++u) t += red[u];
-        const double old = __hip_atomic_exchange(&o.cpart[blockIdx.x], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double old = __hip_atomic_exchange(&o.cpart[bid], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("" ::"v"(old) : "memory");  // the swap has returned before the ticket
         const int tk = __hip_atomic_fetch_add(o.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = tk == (int)gridDim.x - 1;
+        last = tk == nblk - 1;
     }
     __syncthreads();
     if (!last) return;
     double a = 0.0;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x)
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x)
         a += __hip_atomic_fetch_add(&o.cpart[b], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     a = wave_sum(a);
     __syncthreads();
@@ -1172,19 +1175,21 @@ __global__ void __launch_bounds__(UPD_T)
 k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restrict__ node_buf,
             double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
             int update_W, conv_sink o) {
+    // one nonant per grid row (blockIdx.y): the per-nonant index loads of a scenario's
+    // thread run in parallel instead of one dependent chain per nonant (config 2, 30
+    // nonants: 27 us -> a few)
     const int64_t S = st.S;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.y;
     double acc = 0.0;
-    if (s < S) {
-        for (int k = 0; k < st.nn; ++k) {
-            const int d = st.nonant_depth[k];
-            const int gnode = st.node_of[IX(d)];
-            const double xb = node_buf[gnode * st.nlen_max + st.nonant_off[k]];
-            const double xv = x[IX(st.nonant_col[k])];
-            xbar[IX(k)] = xb;
-            if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
-            acc += fabs(xv - xb);
-        }
+    if (s < S && k < st.nn) {
+        const int d = st.nonant_depth[k];
+        const int gnode = st.node_of[IX(d)];
+        const double xb = node_buf[gnode * st.nlen_max + st.nonant_off[k]];
+        const double xv = x[IX(st.nonant_col[k])];
+        xbar[IX(k)] = xb;
+        if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
+        acc += fabs(xv - xb);
     }
     conv_last_block(acc, o);
 }
@@ -1972,7 +1977,9 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
                 ALLOC(h->xp_dirty[k], nch);
             }
         }
-        ALLOC(h->cpart_blk, (Sz + 15) / 16 + 1);  // one per block of the widest grid (path-6 lane groups of 16)
+        // one per block of the widest grid (path-6 lane groups of 16; k_ph_update's nonant x
+        // scenario-block grid)
+        ALLOC(h->cpart_blk, std::max<size_t>((Sz + 15) / 16 + 1, (size_t)std::max(nn, 1) * ((Sz + UPD_T - 1) / UPD_T) + 1));
         ALLOC(h->blk_cnt, 4);
         if (hipMemset(h->blk_cnt, 0, 4 * sizeof(int32_t)) != hipSuccess) {
             phgpu_destroy(h);
@@ -2789,7 +2796,11 @@ static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipS
         }
     }
     if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
-    hipLaunchKernelGGL(k_xbar_partial, grid_for(h->S), dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
+    {
+        dim3 g = grid_for(h->S);
+        g.y = (unsigned)std::max(h->nn, 1);
+        hipLaunchKernelGGL(k_xbar_partial, g, dim3(BLOCK), 0, st, *h, x, node_buf, h->xbar_mixed ? 0 : 1);
+    }
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2860,7 +2871,7 @@ extern "C" int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double*
     const int rc = make_sink(h, conv_local, stats_out, st, o);
     if (rc) return rc;
     // one launch: x̄ scatter, W update, conv (last-block reduction) and the statistics
-    hipLaunchKernelGGL(k_ph_update, dim3((unsigned)((h->S + UPD_T - 1) / UPD_T)), dim3(UPD_T), 0, st, *h, x,
+    hipLaunchKernelGGL(k_ph_update, dim3((unsigned)((h->S + UPD_T - 1) / UPD_T), (unsigned)std::max(h->nn, 1)), dim3(UPD_T), 0, st, *h, x,
                        node_buf, xbar, W, rho, update_W ? 1 : 0, o);
     HIPCHK(hipGetLastError());
     return 0;
