@@ -322,7 +322,9 @@ int phgpu_ipm_info(phgpu_handle h, double* info);
  * rl m | ru m]: bit 0 the same value in every scenario, bit 1 finite in some scenario,
  * bit 2 finite in every scenario, bit 3 (rl elements) rl == ru in every scenario; v0 the
  * first scenario's value.  nonant_slot[n]: nonant index of each column or -1; lanes: lanes
- * per scenario of the IPM kernel (1, 2, 4, 8 or 16).  Writes the
+ * per scenario of the IPM kernel (1, 2, 4, 8 or 16), or threads of a workgroup per scenario
+ * (64, 128, 192 or 256: the subtree kernel for a block-angular pattern unless
+ * PHGPU_IPM_BLK=0, else the workgroup kernel).  Writes the
  * NUL-terminated source to buf when len exceeds its length; returns the length + 1 (or a
  * negative error); info[4] (may be NULL) = {rows in the normal equations, factor entries,
  * factorisation flops, solve flops}. */
