@@ -1,5 +1,6 @@
-"""Prototype of path 7's factorisation (TOOL, not product code): the normal equations
-M = A D A' + E of one scenario factored LDL' by one wave of 64 lanes.
+"""Prototype of the workgroup interior point's factorisation (TOOL, not
+product code): the normal equations M = A D A' + E of one scenario factored LDL' by one
+wave of 64 lanes.
 
 The elimination tree (minimum-degree order, solve_ipm.inc ipm_analyse) is cut below a
 small top set R (<= RMAX rows, upward closed): the rest falls into independent subtrees
