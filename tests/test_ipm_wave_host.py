@@ -132,6 +132,9 @@ def test_blk_plan_shapes():
         b = farmer.batch_creator(farmer.scenario_names_creator(2), crops_multiplier=cm, num_scens=2)
         src = _src_kernel(b, lanes)
         assert "k_solve_ipm_blk" in src and f"#define WT {lanes}\n" in src
+        # the ordering's tie-break leaves the acreage row alone at the root: one root row,
+        # every crop a two-row subtree of four columns, no free columns
+        assert "#define NRT 1\n" in src and "#define NLC 4\n" in src and "#define NLRW 2\n" in src
     # 40 rows in a chain (row i on columns i and i + 1): the elimination tree is a path, one
     # subtree of 40 rows -- too big for a thread, and no small root set splits it
     m, n = 40, 41
