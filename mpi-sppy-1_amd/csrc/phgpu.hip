@@ -123,6 +123,8 @@ struct phgpu_state {
     // wave w takes cw_slc[cw_ptr[w] .. cw_ptr[w+1]) (rw_* for rows)
     int32_t *cw_ptr, *cw_slc, *rw_ptr, *rw_slc;
     int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
+    double* split_part;            // grid-sum partials of the split streaming form ([2][blocks][8])
+    int split_blocks;              // its capacity in blocks
     int32_t* sk_bins;              // [2 parities][2][ORDER_BINS] counting-sort histogram / fill counters (path 2)
     int order_parity;              // which half of sk_bins the next register-path solve uses
     int warm_rec;                  // the warm start lives in the records pk (paths 2r, 3), else in x / y
@@ -2435,6 +2437,14 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         if (per_cu < 1) per_cu = 1;
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > (h->S + B - 1) / B) nblk = (h->S + B - 1) / B;
+        // PHGPU_STREAM_SPLIT=T: the T longest scenarios of the previous solve run first, each
+        // over the whole GPU (the split form of k_solve_stream, cooperative launch), then the
+        // rest on the queue
+        const char* spe = getenv("PHGPU_STREAM_SPLIT");
+        int T = spe ? atoi(spe) : 0;
+        if (T < 0) T = 0;
+        if (T > 16) T = 16;
+        if (T > h->S) T = (int)h->S;
         HIPCHK(hipMemsetAsync(h->qhead, 0, sizeof(int), st));
         // queue order: longest first by the previous solve's iteration counts (the launch
         // ends with its slowest scenario; starting it first shortens the tail)
@@ -2443,12 +2453,36 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             hipLaunchKernelGGL(k_stream_order, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
         else
             hipLaunchKernelGGL(k_stream_order_identity, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
+        if (T > 0) {
+            int occ = 0;
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_solve_stream<1, true>, SBLK, 0));
+            // enough waves for one slice each in the longer pass, never more than fit at once
+            int G = (std::max(h->nsl_c, h->nsl_r) + SWAVES - 1) / SWAVES;
+            G = std::min(G, std::max(occ, 1) * h->num_cus);
+            G = std::max(G, 1);
+            if (h->split_blocks < G) {
+                if (h->split_part) HIPCHK(hipFree(h->split_part));
+                h->split_part = nullptr;
+                // partials [2][G][8], then the barrier counter
+                HIPCHK(hipMalloc((void**)&h->split_part, (size_t)(2 * G * 8 + 1) * sizeof(double)));
+                h->split_blocks = G;
+            }
+            HIPCHK(hipMemsetAsync(h->split_part + (size_t)2 * G * 8, 0, sizeof(double), st));
+            phgpu_state hv = *h;
+            int32_t* qh = h->qhead;
+            double* gp = h->split_part;
+            int q0 = T;
+            void* args[] = {&hv, &P, &qh, &x, &y, &obj, &bound, &status, &iters, &q0, &gp};
+            HIPCHK(hipLaunchCooperativeKernel((const void*)k_solve_stream<1, true>, dim3((unsigned)G), dim3(SBLK), args,
+                                              0, st));
+        }
+        nblk = std::min<int64_t>(nblk, std::max<int64_t>((h->S - T + B - 1) / B, 1));
         if (B == 1)
             hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters);
+                               bound, status, iters, T, (double*)nullptr);
         else
             hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters);
+                               bound, status, iters, T, (double*)nullptr);
         HIPCHK(hipGetLastError());
         h->last_stats = nullptr;
         h->last_status = status;
@@ -3005,6 +3039,7 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
                     h->sk_bins, h->cw_ptr, h->cw_slc, h->rw_ptr, h->rw_slc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->split_part) (void)hipFree(h->split_part);
     if (h->jit) {
         if (h->jit->mod) (void)hipModuleUnload(h->jit->mod);
         delete h->jit;

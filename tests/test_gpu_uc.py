@@ -164,3 +164,60 @@ def test_path4_fix_nonants(gpu):
     e.solve(_lib.default_options(), warm=True)
     assert np.all(np.abs(e.host("obj") - o_free) <= 1e-7 * np.maximum(1.0, np.abs(o_free)))
     e.close()
+
+
+@pytest.mark.parametrize("split", [1, 3])
+def test_uc_split_stragglers_vs_highs(gpu, split):
+    """PHGPU_STREAM_SPLIT=T: the T longest scenarios of the previous solve (the first T of
+    the queue order on a cold solve) run over the whole GPU in the split form of the
+    streaming kernel (cooperative launch, grid barriers and grid sums), the rest on the
+    queue: the same objectives as HiGHS, cold and warm."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import uc
+    keep = os.environ.get("PHGPU_STREAM_SPLIT")
+    os.environ["PHGPU_STREAM_SPLIT"] = str(split)
+    try:
+        names = GOLD["names"]
+        b = uc.batch_creator(names, num_scens=GOLD["num_scens"])
+        e = PHEngine(b, device="cuda:0")
+        assert e.shared and e.kernel_info()["path"] == 4
+        want = np.array(GOLD["lp_obj"])
+        for warm in (False, True):
+            e.solve(_lib.default_options(eps_rel=UC_EPS), warm=warm)
+            st, obj, bnd = e.host("status"), e.host("obj"), e.host("bound")
+            assert (st == _lib.OPTIMAL).all(), (warm, st, e.host("iters"))
+            assert np.all(np.abs(obj - want) <= UC_OBJ_REL * np.abs(want)), (warm, obj, want)
+            assert np.all(np.abs(bnd - want) <= UC_OBJ_REL * np.abs(want)), (warm, bnd, want)
+        e.close()
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_STREAM_SPLIT", None)
+        else:
+            os.environ["PHGPU_STREAM_SPLIT"] = keep
+
+
+def test_path4_split_matches_queue_on_aircond(gpu):
+    """The split form against the queue form on aircond (path 4 forced): statuses and
+    objectives agree to the solve tolerance."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import aircond
+    g = GOLDEN["aircond432_rho1"]
+    kw = dict(g["kwargs"])
+    kw["branching_factors"] = g["branching_factors"]
+    b = aircond.batch_creator(g["names"], **kw)
+    res = []
+    for split in (None, "5"):
+        if split:
+            os.environ["PHGPU_STREAM_SPLIT"] = split
+        try:
+            e = PHEngine(b, device="cuda:0", shared=True)
+            assert e.kernel_info()["path"] == 4
+            e.solve(_lib.default_options(eps_rel=1e-8), warm=False)
+            res.append((e.host("status").copy(), e.host("obj").copy()))
+            e.close()
+        finally:
+            os.environ.pop("PHGPU_STREAM_SPLIT", None)
+    assert (res[0][0] == _lib.OPTIMAL).all() and (res[1][0] == _lib.OPTIMAL).all()
+    assert np.allclose(res[0][1], res[1][1], rtol=1e-6, atol=1e-6), (res[0][1], res[1][1])
