@@ -2434,6 +2434,10 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         int& oc = h->occ_cache[B == 1 ? 4 : 5];
         if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, SBLK, 0));
         per_cu = oc;
+        // PHGPU_STREAM_PER_CU=k: launch k workgroups per CU whatever the occupancy query says
+        // (the ones that do not fit wait for a free CU; the queue has no other dependency)
+        const char* pce = getenv("PHGPU_STREAM_PER_CU");
+        if (pce && atoi(pce) > 0) per_cu = std::min(atoi(pce), 8);
         if (per_cu < 1) per_cu = 1;
         int64_t nblk = (int64_t)per_cu * h->num_cus;
         if (nblk > (h->S + B - 1) / B) nblk = (h->S + B - 1) / B;
