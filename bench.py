@@ -636,6 +636,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    # release the handle while the HIP runtime (and a profiler's tool) is still up, not in
+    # PHEngine.__del__ at interpreter teardown (profiles/r04/ac/uc_1.log: SIGSEGV there)
+    e.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -305,7 +305,7 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
-/* Path-6 (interior point) diagnostics: info[13] = {1 if path 6 applies to the pattern,
+/* Path-6 (interior point) diagnostics: info[15] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
  * and 2 if the module failed to compile or load (path 6 is then not the automatic path
  * until new data arrives by phgpu_set_scenarios), 1 if a module is compiled, rows in its normal
@@ -314,7 +314,9 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
  * scenario of its IPM kernel (1, or a lane group of 2..16: more lanes for fewer local
  * scenarios, PHGPU_IPM_LANES pins it; 64..256: threads of a workgroup per scenario), PH
  * steps folded into solve launches so far (phgpu_ph_step_defer), the IPM kernel (0 none
- * compiled, 1 one lane, 2 lane groups, 3 workgroup, 4 subtree)}. */
+ * compiled, 1 one lane, 2 lane groups, 3 workgroup, 4 subtree), and of the last path-6 solve
+ * (synchronises): scenarios the subtree kernel found still jammed after its re-centrings
+ * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
 /* The path-6 source the library generates for a pattern and its data flags (host code

@@ -2471,22 +2471,27 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
                 HIPCHK(hipMalloc((void**)&h->split_part, (size_t)(2 * G * 8 + 1) * sizeof(double)));
                 h->split_blocks = G;
             }
+            // the barrier counter starts at gbase (PHGPU_SPLIT_BAR_BASE: a test starts it just
+            // below 2^32 so that it wraps during the launch; the barrier compares wrap-safe)
+            const char* bbe = getenv("PHGPU_SPLIT_BAR_BASE");
+            unsigned gbase = bbe ? (unsigned)strtoul(bbe, nullptr, 0) : 0u;
             HIPCHK(hipMemsetAsync(h->split_part + (size_t)2 * G * 8, 0, sizeof(double), st));
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(h->split_part + (size_t)2 * G * 8), (int)gbase, 1, st));
             phgpu_state hv = *h;
             int32_t* qh = h->qhead;
             double* gp = h->split_part;
             int q0 = T;
-            void* args[] = {&hv, &P, &qh, &x, &y, &obj, &bound, &status, &iters, &q0, &gp};
+            void* args[] = {&hv, &P, &qh, &x, &y, &obj, &bound, &status, &iters, &q0, &gp, &gbase};
             HIPCHK(hipLaunchCooperativeKernel((const void*)k_solve_stream<1, true>, dim3((unsigned)G), dim3(SBLK), args,
                                               0, st));
         }
         nblk = std::min<int64_t>(nblk, std::max<int64_t>((h->S - T + B - 1) / B, 1));
         if (B == 1)
             hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters, T, (double*)nullptr);
+                               bound, status, iters, T, (double*)nullptr, 0u);
         else
             hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters, T, (double*)nullptr);
+                               bound, status, iters, T, (double*)nullptr, 0u);
         HIPCHK(hipGetLastError());
         h->last_stats = nullptr;
         h->last_status = status;
@@ -3117,7 +3122,7 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     if (!h || !info) return set_err(-1, "null argument");
-    for (int k = 0; k < 13; ++k) info[k] = 0.0;
+    for (int k = 0; k < 15; ++k) info[k] = 0.0;
     info[0] = ipm_eligible(h) ? 1.0 : 0.0;
     info[11] = (double)h->folded;
     info[1] = h->ipm_nf;
@@ -3132,6 +3137,14 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
         info[9] = h->ipm->sol_flops;
         info[10] = h->ipm->L;
         info[12] = h->ipm->L == 1 ? 1 : (h->ipm->L < 64 ? 2 : (h->ipm->blk ? 4 : 3));
+    }
+    // the subtree kernel's jam statistics of the last path-6 solve (synchronous read)
+    if (h->last_stats && h->ipm_stats && h->last_path == 6) {
+        unsigned long long st8[8];
+        if (hipMemcpy(st8, h->last_stats, sizeof(st8), hipMemcpyDeviceToHost) == hipSuccess) {
+            info[13] = (double)st8[6];
+            info[14] = (double)st8[7];
+        }
     }
     return 0;
 }

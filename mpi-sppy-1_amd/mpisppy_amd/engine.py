@@ -11,7 +11,10 @@ GPU, scenario-fastest ``[k, S]``) and sequences the per-PH-iteration work:
 All launches go to torch's current stream; host synchronisation happens only where
 the reference needs a host scalar (the convergence test, bounds).
 """
+import atexit
 import ctypes
+import weakref
+
 import numpy as np
 import torch
 
@@ -40,6 +43,31 @@ def combine_node_partials(comm, node_buf):
 # scenario run on the shared-matrix streaming path (path 4, include/phgpu.h
 # PHGPU_SHARED_MATRIX); smaller ones fit the register / workgroup-resident paths
 SHARED_MIN_SIZE = 8192
+
+
+# Engines still open at interpreter exit are closed by an atexit hook registered when the
+# first engine is made -- after torch's own hooks, so it runs before them (LIFO), while the
+# HIP runtime (and a profiler's tool library) is still up.  PHEngine.__del__ at interpreter
+# teardown could run after them: a rocprofv3 run of bench.py died in it (SIGSEGV after the
+# tool's finalisation, profiles/r04/ac/uc_1.log).
+_LIVE = weakref.WeakSet()
+_ATEXIT = []
+
+
+def close_all():
+    """Close every engine still open (phgpu_destroy after a device synchronise)."""
+    for e in list(_LIVE):
+        try:
+            e.close()
+        except Exception:
+            pass
+
+
+def _track(engine):
+    if not _ATEXIT:
+        atexit.register(close_all)
+        _ATEXIT.append(True)
+    _LIVE.add(engine)
 
 
 def matrix_is_shared(batch):
@@ -91,6 +119,10 @@ class PHEngine:
                                           self.nlen_max, _lib.SHARED_MATRIX if self.shared else 0),
                    "phgpu_create2")
         self.h = h
+        _track(self)
+        # library calls of the PH step, by kind (tests assert which path a loop took)
+        self.calls = {"ph_reduce": 0, "ph_update_ex": 0, "ph_step_local": 0, "ph_step_defer": 0,
+                      "allreduce_xbar": 0, "allreduce_conv_side": 0}
         dev = self.device
         self.A_val = _dev_T(b.A_val[0] if self.shared else b.A_val, dev)
         self.c = _dev_T(b.c, dev)
@@ -143,6 +175,7 @@ class PHEngine:
         self._conv_seq = 0        # the update whose conv the pending readback returns
         self._conv_seen = 0       # the last update whose conv (and statistics) the host has seen
         self._side = None         # side stream of the conv all-reduce (several ranks)
+        self._conv_ev = None      # the event behind its copy to pinned memory
         self._wait_stats = None   # the pinned statistics row the pending update writes (one rank)
         # markers: the event behind an update (by update number), recorded lazily, only when
         # the host needs an update's statistics before its conv arrived
@@ -169,8 +202,11 @@ class PHEngine:
         if getattr(self, "h", None) is not None and self.h.value:
             self._flush_step()
             torch.cuda.synchronize(self.device)
+            if getattr(self, "_side", None) is not None:
+                self._side.synchronize()
             self.lib.phgpu_destroy(self.h)
             self.h = None
+        _LIVE.discard(self)
 
     def __del__(self):
         try:
@@ -191,10 +227,10 @@ class PHEngine:
 
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
-        info = (ctypes.c_double * 13)()
+        info = (ctypes.c_double * 15)()
         _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
         keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
-                "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel"]
+                "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel", "jam_handovers", "recentrings"]
         return dict(zip(keys, list(info)))
 
     # -------------------------------------------------------------- PH state
@@ -412,6 +448,7 @@ class PHEngine:
         return int(st[1:4].sum())
 
     def compute_xbar_partials(self):
+        self.calls["ph_reduce"] += 1
         _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self.x), _ptr(self.node_buf), self._stream()),
                    "phgpu_ph_reduce")
         return self.node_buf
@@ -426,6 +463,8 @@ class PHEngine:
             return None
         self._xbar_pending = False
         self.compute_xbar_partials()
+        if self.comm.size > 1:
+            self.calls["allreduce_xbar"] += 1
         self._allreduce_sum_(self.node_buf)
         return self.node_buf
 
@@ -448,6 +487,10 @@ class PHEngine:
         them there).  ``defer`` (one rank, x̄ pending: PHBase.iterk_loop's speculative
         step) hands the step to phgpu_ph_step_defer, which folds it into the next solve
         launch when it can; the solve must follow before anything reads W."""
+        if self._upd_seq > self._conv_seen and self._conv_zero_copy:
+            # the previous update's conv / statistics were never read back: its kernel may
+            # still store into the pinned words after the sentinels below are set (ADVICE r4)
+            torch.cuda.current_stream(self.device).synchronize()
         self._conv_zero_copy = self.comm.size == 1
         conv = self._conv_host if self._conv_zero_copy else self.conv_buf
         self._conv_np[0] = float("nan")     # the readback's sentinel (before the launch)
@@ -470,11 +513,13 @@ class PHEngine:
         if getattr(self, "_xbar_pending", False):
             self._xbar_pending = False
             fn = self.lib.phgpu_ph_step_defer if defer else self.lib.phgpu_ph_step_local
+            self.calls["ph_step_defer" if defer else "ph_step_local"] += 1
             _lib.check(fn(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
                           _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
                           _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_step")
             self._step_deferred = bool(defer)
             return
+        self.calls["ph_update_ex"] += 1
         _lib.check(self.lib.phgpu_ph_update_ex(self.h, _ptr(self.x), _ptr(self.node_buf), _ptr(self.xbar),
                                                _ptr(self.W), _ptr(self.rho), 1 if update_W else 0,
                                                _ptr(conv), _ptr(stats), self._stream()), "phgpu_ph_update_ex")
@@ -500,9 +545,17 @@ class PHEngine:
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
         self._side.wait_event(ev)
+        self.calls["allreduce_conv_side"] += 1
         with torch.cuda.stream(self._side):
             self._allreduce_sum_(self.conv_buf, tag="overlapped")
             self._conv_host.copy_(self.conv_buf, non_blocking=True)
+            # the host waits for this event, not for the word to change: the copy engine may
+            # write the 8 bytes piecewise, and a poll caught a half-written value (its top
+            # byte still the NaN sentinel's: 9.4e306 as conv on one rank, round-5 2-rank
+            # test), which could make ranks disagree on the break and deadlock
+            if self._conv_ev is None:
+                self._conv_ev = torch.cuda.Event()
+            self._conv_ev.record(self._side)
 
     _SPIN = 200000
 
@@ -511,7 +564,12 @@ class PHEngine:
         streams, which also surfaces a device error)."""
         self._flush_step()          # a deferred step no solve has taken yet: run it now
         a = self._conv_np
-        st = self._wait_stats if self._conv_zero_copy else None
+        if not self._conv_zero_copy:
+            # several ranks: the side stream's copy is complete once its event is
+            self._conv_ev.synchronize()
+            self._conv_seen = max(self._conv_seen, self._conv_seq)
+            return float(a[0]) / self.comm.size
+        st = self._wait_stats
         n = 0
         while a[0] != a[0] or (st is not None and (st == -1).any()):
             n += 1

@@ -124,10 +124,11 @@ class _Params(ctypes.Structure):
 
 
 def solve(batch, lanes=64, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e-12, max_ipm=80, eps_tight=1e-13,
-          x_in=None, y_in=None):
+          x_in=None, y_in=None, stats=None):
     """Solve every scenario of a ScenarioBatch with the host-run workgroup kernel (lanes =
     its threads per scenario, 64 WPS).  Returns x [S, n], y [S, m], obj, bound, status
-    (-1 = left for the fallback), iters."""
+    (-1 = left for the fallback), iters.  ``stats`` (a list): the kernel's 8 statistics
+    words are appended to it."""
     import mpisppy_amd._lib as L
     src, _ = L.ipm_source(batch, lanes)
     assert "#define WT " + str(lanes) in src, "the generator chose another workgroup size"
@@ -169,6 +170,8 @@ def solve(batch, lanes=64, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e
     keep.append(st16)
     p.stats, p.stats_zero = st16.ctypes.data, st16[8:].ctypes.data
     lib.wave_run(ctypes.byref(p), S)
+    if stats is not None:
+        stats.append(st16[:8].copy())
     st = status.copy()
     st[fl[:cnt[0]]] = -1
     return out["x"].T.copy(), out["y"].T.copy(), obj, bound, st, iters

@@ -199,7 +199,9 @@ def test_uc_split_stragglers_vs_highs(gpu, split):
 
 def test_path4_split_matches_queue_on_aircond(gpu):
     """The split form against the queue form on aircond (path 4 forced): statuses and
-    objectives agree to the solve tolerance."""
+    objectives agree to the solve tolerance -- also with the grid barrier's counter started
+    4,096 below 2^32 (PHGPU_SPLIT_BAR_BASE), so that it wraps within the first scenario
+    (the barrier compares the signed distance to its target)."""
     from mpisppy_amd import _lib
     from mpisppy_amd.engine import PHEngine
     from mpisppy_amd.examples import aircond
@@ -208,9 +210,11 @@ def test_path4_split_matches_queue_on_aircond(gpu):
     kw["branching_factors"] = g["branching_factors"]
     b = aircond.batch_creator(g["names"], **kw)
     res = []
-    for split in (None, "5"):
+    for split, base in ((None, None), ("5", None), ("5", hex(2**32 - 4096))):
         if split:
             os.environ["PHGPU_STREAM_SPLIT"] = split
+        if base:
+            os.environ["PHGPU_SPLIT_BAR_BASE"] = base
         try:
             e = PHEngine(b, device="cuda:0", shared=True)
             assert e.kernel_info()["path"] == 4
@@ -219,5 +223,9 @@ def test_path4_split_matches_queue_on_aircond(gpu):
             e.close()
         finally:
             os.environ.pop("PHGPU_STREAM_SPLIT", None)
-    assert (res[0][0] == _lib.OPTIMAL).all() and (res[1][0] == _lib.OPTIMAL).all()
-    assert np.allclose(res[0][1], res[1][1], rtol=1e-6, atol=1e-6), (res[0][1], res[1][1])
+            os.environ.pop("PHGPU_SPLIT_BAR_BASE", None)
+    for st, ob in res[1:]:
+        assert (res[0][0] == _lib.OPTIMAL).all() and (st == _lib.OPTIMAL).all()
+        assert np.allclose(res[0][1], ob, rtol=1e-6, atol=1e-6), (res[0][1], ob)
+    # the wrapped-counter run takes the same branches: bit-identical to the plain split run
+    assert np.array_equal(res[1][1], res[2][1])
