@@ -572,7 +572,8 @@ def main():
     comm.allreduce_sum_(n_bad)
     kinfo = e.kernel_info()
     ws = e.workspace_bytes() + 8 * (b.S * (b.n + b.m + 3 * max(b.nn, 1) + 4))
-    rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir, ipm=e.ipm_info())
+    ipm_diag = e.ipm_info()
+    rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir, ipm=ipm_diag)
     ph_its = 1.0 / med               # median of iterations 2..K
     if rank == 0:
         out = {
@@ -622,6 +623,11 @@ def main():
             # every timed solve: scenarios not OPTIMAL (summed over ranks), and the last one
             "not_optimal_per_timed_solve_max": int(bad_timed.max().item()),
             "all_optimal": bool(n_bad.item() == 0 and bad_timed.max().item() == 0),
+            # the subtree kernel (config 2): scenarios of the last timed solve found still
+            # jammed after their re-centrings -- handed to the PDHG fallback, not reported
+            # OPTIMAL -- and its re-centrings
+            "path6_last_solve_jam_handovers": int(ipm_diag.get("jam_handovers", 0)),
+            "path6_last_solve_recentrings": int(ipm_diag.get("recentrings", 0)),
             "iter0_not_optimal": iter0_bad,
             "iter0_relaxed_resolve": iter0_relaxed,
             # every Iter0 solve met the KKT tolerance: the trivial bound is the Lagrangian dual

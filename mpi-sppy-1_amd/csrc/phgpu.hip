@@ -2547,7 +2547,8 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         // slower, 8,192 scenarios 0.095 ms per PH iteration against 0.079 as its own launch,
         // profiles/r04/o/; PHGPU_FUSE_STEP=1 folds there too)
         const bool fuse = path == 6 && defer && !(fe && atoi(fe) == 0) && q.stream == st && q.x != x &&
-                          (h->ipm && (h->ipm->L == 1 || (fe && atoi(fe) == 1))) &&
+                          // (the workgroup kernels, L >= 64, carry no folded step at all)
+                          (h->ipm && (h->ipm->L == 1 || (fe && atoi(fe) == 1 && h->ipm->L < 64))) &&
                           h->nb_idx && h->xbar_single && h->xbar_mixed == 0 && h->nn > 0 && h->nn <= XL_NN_MAX &&
                           xp_valid(h, q.x) && q.W == h->W && q.xbar == h->xbar && q.rho == h->rho &&
                           (!q.stats || (stats_keep && stats_keep == h->ipm_stats + 8 * (1 - h->ipm_parity)));

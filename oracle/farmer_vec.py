@@ -113,8 +113,14 @@ def crop_cost(bp, sl, f0, x):
     return f0 + (sl * seg).sum(-1)
 
 
-def iter0_lp(bp, sl, f0, total):
-    """Exact Iter0 LP: fractional knapsack over the negative-slope segments."""
+def iter0_lp(bp, sl, f0, total, ties="symmetric"):
+    """Exact Iter0 LP: fractional knapsack over the negative-slope segments.
+
+    ``ties``: the point taken on an optimal face (exact slope ties, below): "symmetric"
+    (the analytic-centre point an interior-point solve converges to, the fixtures' choice)
+    or "vertex" (the stable slope order fills the first tied segment first -- a basic
+    solution, what a simplex solver such as the reference's would return).  The objective
+    and every tied group's total acreage are the same either way."""
     S, K, J = sl.shape
     length = np.diff(bp, axis=-1).reshape(S, K * J)
     slope = sl.reshape(S, K * J)
@@ -127,9 +133,11 @@ def iter0_lp(bp, sl, f0, total):
     # the optimum is a face, not a vertex): the acreage a tied group receives is split over
     # its segments in proportion to their lengths -- for identical copies the symmetric
     # point of the face, the solution an interior-point solve (the analytic centre) or a
-    # PDHG solve from a symmetric start converges to.  The objective is unchanged.
+    # PDHG solve from a symmetric start converges to.  The objective is unchanged.  The
+    # reference's own point there depends on its solver (a simplex basis: ties="vertex"),
+    # and so does every later PH iterate of a batch holding these scenarios.
     tied = (np.diff(sl_o, axis=1) == 0.0) & (len_o[:, 1:] > 0.0) & (len_o[:, :-1] > 0.0)
-    for s in np.nonzero(tied.any(1))[0]:
+    for s in (np.nonzero(tied.any(1))[0] if ties == "symmetric" else []):
         k = 0
         while k < K * J:
             e = k + 1
@@ -244,7 +252,7 @@ def _prox_breakpoints(bp, sl, f0, W, xbar, rho, total, chunk_elems=1 << 24):
 class FarmerVecPH:
     """Single-rank PH on the vectorised farmer solvers (phbase.py:758-979)."""
 
-    def __init__(self, names, cm, rho=1.0, num_scens=None, seedoffset=0):
+    def __init__(self, names, cm, rho=1.0, num_scens=None, seedoffset=0, ties="symmetric"):
         self.names = list(names)
         self.cm = cm
         self.total = 500.0 * cm
@@ -256,9 +264,10 @@ class FarmerVecPH:
         self.W = np.zeros((self.S, self.K))
         self.xbar = np.zeros((self.S, self.K))
         self.history = []
+        self.ties = ties
 
     def iter0(self):
-        self.x, self.obj = iter0_lp(self.bp, self.sl, self.f0, self.total)
+        self.x, self.obj = iter0_lp(self.bp, self.sl, self.f0, self.total, ties=self.ties)
         self.iter0_x = self.x.copy()
         self.iter0_obj = self.obj.copy()
         self.trivial_bound = math.fsum(self.prob * self.obj)        # spopt.py:346-391

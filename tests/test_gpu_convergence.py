@@ -89,6 +89,11 @@ def _run_convergence(path, eps_rel, w_tol):
     seen = _record_conv(ph)
     ph.iterk_loop()
     assert ph._speculate(False), "the bench's loop variant (speculative solve) must be the one tested"
+    if path == 6:
+        # the bench's exact variant: the one-rank PH step folded into the one-lane solve
+        # launch on every iteration that solved
+        ii = ph.engine.ipm_info()
+        assert ii["lanes"] == 1 and ii["folded_steps"] >= ph._PHIter - 2, ii
     assert ph.converged
     k = ph._PHIter
     want = CONV["breaks"]["0.001"]

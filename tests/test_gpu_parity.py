@@ -98,9 +98,10 @@ def test_farmer_cm10_parity(gpu, kernel):
     the exact oracle after 5 PH iterations; batch_creator path.  scen3..18: for
     scen0..2 the cm copies of a crop are identical, so their Iter0 LP has a whole
     optimal face and only the objective (trivial bound) is solver-independent.
-    kernel 0 (auto) takes path 6's workgroup interior point (one wave per scenario,
-    jit_ipm_wave.hip.in); kernel 3 the workgroup PDHG (one wave per scenario, the 30-entry
-    acreage row as a long row); kernel 2 the wide-row register instance."""
+    kernel 0 (auto) takes path 6's subtree interior point (k_solve_ipm_blk, one wave per
+    scenario, jit_ipm_blk.hip.in: the block-angular pattern's automatic choice); kernel 3 the
+    workgroup PDHG (one wave per scenario, the 30-entry acreage row as a long row); kernel 2
+    the wide-row register instance."""
     from mpisppy_amd.examples import farmer
     g = GOLD["farmer16_cm10_rho1"]
     names = g["names"]
@@ -112,6 +113,7 @@ def test_farmer_cm10_parity(gpu, kernel):
     if kernel == 0:
         ii = ph.engine.ipm_info()
         assert info["path"] == 6 and ii["lanes"] == 64 and ii["scratch_bytes"] == 0, (info, ii)
+        assert ii["kernel"] == 4, ii    # the subtree kernel, not the workgroup one (3)
     else:
         assert info["wps"] == 1 and (info["wZC"], info["wZR"]) == (3, 4), info
         assert info["instance"] >= 0 and info["lanes"] == 64 and info["ZR"] >= 30, info

@@ -82,17 +82,40 @@ def _bench_path(ph):
     return ph.engine.kernel_info()["path"]
 
 
+def _group_sums(v, cm):
+    """Per base crop, the sum over its cm copies (nonant order: crops sorted by name)."""
+    from oracle.farmer_vec import crops_sorted
+    bases = [c.rstrip("0123456789") for c in crops_sorted(cm)]
+    return np.array([sum(v[k] for k, b in enumerate(bases) if b == g) for g in ("CORN", "SUGAR_BEETS", "WHEAT")])
+
+
 def test_config2_farmer1024_cm10_bound(gpu):
     """Config 2 on the path bench.py times (the automatic choice): trivial bound, sampled
     Iter0 objectives, x̄ and conv of 5 PH iterations, every 8th scenario's W and E[obj]
-    after them, for scen0..scen1023 at cm = 10."""
+    after them, for scen0..scen1023 at cm = 10.  scen0..2's Iter0 optimum is a face (tied
+    crop copies): the first x̄'s per-crop group sums are the solver-independent check
+    (test_oracle_scale.py::test_tied_face_group_sums_are_solver_independent); the per-copy
+    values and the later iterates are pinned to the symmetric point of that face, the one
+    an interior point converges to (a simplex solver, the reference's, returns a vertex)."""
     g = SCALE["farmer1024_cm10"]
     assert g["ph_iters"] == 5
     names = [f"scen{i}" for i in range(1024)]
     from mpisppy_amd.examples import farmer
     ph = _farmer_ph(names, 10, 1024, iterk_solver_options=dict(farmer.PDHG_ITERK_OPTIONS))
+    first = []
+    conv_diff = ph.convergence_diff
+
+    def keep_first():
+        v = conv_diff()
+        if not first:
+            first.append(ph.xbar_by_node()["ROOT"][:30].copy())
+        return v
+    ph.convergence_diff = keep_first
     _run_and_compare(ph, g)
-    print("config 2 path", _bench_path(ph), ph.engine.kernel_info())
+    assert np.abs(_group_sums(first[0], 10) - _group_sums(np.array(g["xbar"][0]), 10)).max() <= ABS
+    # the bench's kernel: path 6, the subtree interior point (k_solve_ipm_blk), no scratch
+    ii = ph.engine.ipm_info()
+    assert _bench_path(ph) == 6 and ii["kernel"] == 4 and ii["scratch_bytes"] == 0, (ph.engine.kernel_info(), ii)
 
 
 @pytest.mark.parametrize("thr", ["0.01"])

@@ -24,7 +24,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _farmer(S, spec, thresh, kernel=0):
+def _farmer(S, spec, thresh, kernel=0, cm=1):
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     so = {"kernel": kernel} if kernel else {}
@@ -33,7 +33,7 @@ def _farmer(S, spec, thresh, kernel=0):
             "batch_creator": farmer.batch_creator, "speculative_solve": spec,
             "iter0_solver_options": dict(so), "iterk_solver_options": dict(so)}
     return PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
-              scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": S})
+              scenario_creator_kwargs={"crops_multiplier": cm, "num_scens": S})
 
 
 def _aircond(spec, thresh):
@@ -64,6 +64,7 @@ def _run(make, spec):
     out["x_after"] = e.x.cpu().numpy().copy()
     out["iters_after"] = e.iters.cpu().numpy().copy()
     out["kernel"] = e.kernel_info()
+    out["ipm"] = e.ipm_info()
     return out
 
 
@@ -72,6 +73,8 @@ CASES = {
     "farmer4096_record_mode": lambda spec: _farmer(4096, spec, 3e-2),
     "farmer4096_ipm": lambda spec: _farmer(4096, spec, 3e-2),
     "farmer256_global_kernel": lambda spec: _farmer(256, spec, 3e-2, kernel=1),
+    # config 2's pattern (cm = 10): the subtree interior point, which never folds the step
+    "farmer128_cm10_subtree": lambda spec: _farmer(128, spec, 3e-2, cm=10),
     "aircond432": lambda spec: _aircond(spec, 1e-4),
 }
 
@@ -98,6 +101,8 @@ def test_speculative_solve_is_invisible(gpu, case):
         assert a["kernel"]["rec"] == 1, a["kernel"]
     if case == "farmer4096_ipm":
         assert a["kernel"]["path"] == 6, a["kernel"]
+    if case == "farmer128_cm10_subtree":
+        assert a["kernel"]["path"] == 6 and a["ipm"]["kernel"] == 4 and a["ipm"]["folded_steps"] == 0, a
     assert a["iter"] == b["iter"] and a["conv"] == b["conv"], (a["iter"], b["iter"], a["conv"], b["conv"])
     for k in ("W", "xbar", "node_buf", "x", "x_after", "iters_after"):
         assert np.array_equal(a[k], b[k]), (case, k, np.abs(a[k] - b[k]).max())
@@ -139,3 +144,25 @@ def test_folded_step_matches_the_step_launch(gpu, S):
     for k in ("W", "xbar", "node_buf", "x"):
         scale = max(1.0, float(np.abs(b[k]).max()))
         assert np.abs(a[k] - b[k]).max() <= 1e-8 * scale, (k, np.abs(a[k] - b[k]).max())
+
+
+def test_subtree_kernel_never_folds_the_step(gpu):
+    """PHGPU_FUSE_STEP=1 asks the library to fold the one-rank PH step into lane-group
+    launches too; the workgroup kernels (config 2's subtree interior point) carry no folded
+    step, so the step must still run as its own launch there: same iterations and bits as
+    the unforced run, folded_steps 0."""
+    keep = os.environ.get("PHGPU_FUSE_STEP")
+    try:
+        os.environ.pop("PHGPU_FUSE_STEP", None)
+        b = _run(lambda spec: _farmer(128, spec, 3e-2, cm=10), True)
+        os.environ["PHGPU_FUSE_STEP"] = "1"
+        a = _run(lambda spec: _farmer(128, spec, 3e-2, cm=10), True)
+    finally:
+        if keep is None:
+            os.environ.pop("PHGPU_FUSE_STEP", None)
+        else:
+            os.environ["PHGPU_FUSE_STEP"] = keep
+    assert a["ipm"]["kernel"] == 4 and a["ipm"]["folded_steps"] == 0, a["ipm"]
+    assert a["iter"] == b["iter"] and a["conv"] == b["conv"]
+    for k in ("W", "xbar", "x"):
+        assert np.array_equal(a[k], b[k]), k

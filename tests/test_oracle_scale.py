@@ -62,6 +62,37 @@ def test_vec_lp_tied_copies_take_the_symmetric_point(cm):
         assert x[s].sum() <= 500.0 * cm + 1e-9
 
 
+def _group_sums(x, cm):
+    """Per base crop, the sum over its cm copies (the face-invariant part of a tied x)."""
+    bases = [c.rstrip("0123456789") for c in fv.crops_sorted(cm)]
+    return np.stack([x[..., [k for k, b in enumerate(bases) if b == g]].sum(-1) for g in ("CORN", "SUGAR_BEETS",
+                                                                                          "WHEAT")], -1)
+
+
+def test_tied_face_group_sums_are_solver_independent():
+    """Config 2's scen0..2 (cm = 10, identical crop copies): a simplex basis (ties="vertex",
+    what the reference's solvers return) and the symmetric point (ties="symmetric", the
+    fixtures' and the interior point's) have the same objective and the same acreage per
+    base crop, but different per-copy acreage -- so x̄ per copy after Iter0 is pinned only
+    up to the face, and its per-crop group sums are the solver-independent comparison
+    (tests/test_gpu_scale.py config 2 checks both).  Every later PH iterate depends on the
+    choice (W per copy), which is why farmer_scale.json records the symmetric one."""
+    warnings.simplefilter("ignore")
+    names = [f"scen{i}" for i in range(1024)]
+    bp, sl, f0 = fv.pieces(fv.yields(names, 10), 10)
+    xs, os_ = fv.iter0_lp(bp, sl, f0, 5000.0, ties="symmetric")
+    xv, ov = fv.iter0_lp(bp, sl, f0, 5000.0, ties="vertex")
+    assert np.array_equal(xs[3:], xv[3:])               # no ties beyond scen0..2
+    assert np.abs(os_ - ov).max() <= 1e-9 * np.abs(os_).max()
+    assert np.abs(_group_sums(xs, 10) - _group_sums(xv, 10)).max() <= 1e-9
+    assert np.abs(xs[:3] - xv[:3]).max() > 1.0           # the face is real
+    xbar_s, xbar_v = xs.mean(0), xv.mean(0)
+    assert np.abs(_group_sums(xbar_s, 10) - _group_sums(xbar_v, 10)).max() <= 1e-12 * 5000
+    # the fixture's first x̄ is the symmetric choice
+    g = SCALE["farmer1024_cm10"]
+    assert np.abs(np.array(g["xbar"][0]) - xbar_s).max() <= 1e-9
+
+
 @pytest.mark.parametrize("cm", [1, 10])
 def test_vec_prox_matches_exact(cm):
     names = [f"scen{i}" for i in range(3, 23)]

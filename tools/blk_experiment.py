@@ -86,7 +86,7 @@ def main():
                   f"fail {(~ok).sum()} jam {int(st8[0][6])} recentre {int(st8[0][7])} "
                   f"max|x-oracle| (solved) {err[ok].max():.2e}  tail {tail}", flush=True)
             if a.trace == k + 1:
-                i = int(np.argmax(it))
+                i = int(np.argmax(st != 0)) if (st != 0).any() else int(np.argmax(it))
                 tsrc = "#include <stdio.h>\n#define WTRACE(...) if (threadIdx.x == 0) printf(__VA_ARGS__)\n" + src
                 L.ipm_source = lambda batch, lanes=1: (tsrc, None)  # noqa: E731
                 one = farmer.batch_creator([names[sub[i]]], crops_multiplier=a.cm, num_scens=a.S)

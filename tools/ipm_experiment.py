@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--ref", default=None)
     ap.add_argument("--warm", action="store_true", help="pass the previous x / y as x_in / y_in")
     ap.add_argument("--worst", type=int, default=0, help="print the slowest scenarios of this PH iteration")
+    ap.add_argument("--trace", default=None, help="K:S -- print scenario S's iterations in PH iteration K")
     a = ap.parse_args()
     import ipm_host
     import mpisppy_amd._lib as L
@@ -59,6 +60,9 @@ def main():
             src = src[:k] + line + src[k:]
     orig = L.ipm_source
     L.ipm_source = lambda batch, lanes=1: (src, None)  # noqa: E731
+    tk, ts = (int(v) for v in a.trace.split(":")) if a.trace else (-1, -1)
+    k = src.index("\n", src.index("#define IPM_GAM")) + 1
+    tsrc = src[:k] + f"#define WTRACE(...) if (s == {ts}) printf(__VA_ARGS__)\n" + src[k:]
     try:
         nn = b.nn
         nc = b.nonant_col
@@ -76,6 +80,7 @@ def main():
                 den = np.bincount(g, prob)
                 xbar[:, kk] = (num / np.where(den > 0, den, 1))[g]
             W = W + rho * (x[:, nc] - xbar)
+            L.ipm_source = (lambda batch, lanes=1: (tsrc, None)) if k + 1 == tk else (lambda batch, lanes=1: (src, None))
             x, y, obj, bound, st, it = ipm_host.solve(b, W=W, rho=rho, xbar=xbar, eps_rel=a.eps,
                                                       eps_tight=a.eps_tight,
                                                       x_in=x if a.warm else None, y_in=y if a.warm else None)
