@@ -630,6 +630,9 @@ def main():
             "path6_last_solve_recentrings": int(ipm_diag.get("recentrings", 0)),
             "iter0_not_optimal": iter0_bad,
             "iter0_relaxed_resolve": iter0_relaxed,
+            # path 4 (config 5): warm continuation solves of Iter0 LPs left at the PDHG cap
+            # (PHBase._iter0_continue: the stragglers over the whole GPU), before the bound
+            "iter0_continuation_solves": int(getattr(ph, "iter0_continued", 0)),
             # every Iter0 solve met the KKT tolerance: the trivial bound is the Lagrangian dual
             # bound with projected reduced costs (PDLP convention), accurate to that
             # tolerance -- not an exact certificate; an Iter0 solve at the

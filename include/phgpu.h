@@ -96,6 +96,10 @@ typedef struct {
                               checks from this iteration on (< 0: never)      [512] */
     double eps_infeas;     /* certificate tolerance: ray violation <= eps * |ray
                               objective| (PDLP-style)      [1e-8] */
+    int32_t split_longest; /* path 4: the split_longest (<= 16) scenarios with the most
+                              iterations in the previous solve run first, each over the
+                              whole GPU (the split form); 0: the
+                              PHGPU_STREAM_SPLIT environment variable, else none  [0] */
 } phgpu_options;
 /* max_iter must be a multiple of restart_every: the register-resident kernel counts
  * iterations in chunks of restart_every and stops exactly at max_iter (both kernels then

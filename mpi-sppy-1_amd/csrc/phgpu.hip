@@ -1769,6 +1769,7 @@ extern "C" int phgpu_default_options(phgpu_options* o) {
     o->kernel = 0;
     o->infeas_start = 512;
     o->eps_infeas = 1e-8;
+    o->split_longest = 0;
     return 0;
 }
 
@@ -2445,7 +2446,7 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         // over the whole GPU (the split form of k_solve_stream, cooperative launch), then the
         // rest on the queue
         const char* spe = getenv("PHGPU_STREAM_SPLIT");
-        int T = spe ? atoi(spe) : 0;
+        int T = o.split_longest > 0 ? o.split_longest : (spe ? atoi(spe) : 0);
         if (T < 0) T = 0;
         if (T > 16) T = 16;
         if (T > h->S) T = (int)h->S;

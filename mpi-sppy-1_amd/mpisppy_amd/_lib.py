@@ -36,6 +36,7 @@ class PhgpuOptions(ctypes.Structure):
         ("kernel", c_i32),
         ("infeas_start", c_i32),
         ("eps_infeas", c_dbl),
+        ("split_longest", c_i32),
     ]
 
 

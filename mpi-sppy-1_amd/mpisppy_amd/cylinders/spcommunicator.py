@@ -2,11 +2,19 @@
 
 The reference gives every cylinder its own MPI ranks and moves W / nonants / bounds
 through one-sided MPI windows carrying a trailing write id (spcommunicator.py:93-120,
-hub.py:345-450, spoke.py:34-118).  Here every cylinder is co-located on every rank's
-GPU (one process per GPU): a window is a device buffer owned by the writer plus a
-host-side write id, and the hub drives the spokes cooperatively from its ``sync``.
-The rank communicator of each cylinder is the same ``Comm`` (torch.distributed), so a
-spoke's reductions go over the same ranks that hold its scenario slice.
+hub.py:345-450, spoke.py:34-118).  WheelSpinner places the cylinders in one of two ways
+(spin_the_wheel.py):
+
+  * "ranks" (the reference's placement): the world splits into n_spokes + 1 cylinders of
+    P ranks each (``fullcomm`` / ``strata_comm`` / ``cylinder_comm`` as in
+    spin_the_wheel.py:219-237); windows are keys of the job's rendezvous store carrying
+    'ci'-ordered W or nonants plus the three trailing slots [outer bound, inner bound,
+    write id] (cylinders/transport.py);
+  * "colocated": every cylinder on every rank's GPU, a window a device buffer plus a
+    host-side write id, the hub driving the spokes from its ``sync``; each cylinder's
+    rank communicator is then the same ``Comm``.
+
+This base class holds the communicators and the hooks the hub and spokes override.
 """
 
 

@@ -11,7 +11,7 @@ solve -> sync).  The per-scenario Python loops become device kernels:
 import time
 import numpy as np
 
-from . import global_toc
+from . import _lib, global_toc
 from .spopt import SPOpt
 
 
@@ -189,6 +189,7 @@ class PHBase(SPOpt):
             relaxed["eps_rel"] = PH_EPS_REL
             self.solve_loop(solver_options=relaxed, dtiming=dtiming, gripe=True, verbose=verbose,
                             warm_start=True)
+        self.iter0_continued = self._iter0_continue(dtiming, verbose)
         self._update_E1()
         if abs(1 - self.E1) > self.E1_tolerance:
             # the reference prints ERROR and calls quit() (phbase.py:812-817)
@@ -230,6 +231,31 @@ class PHBase(SPOpt):
         self.reenable_W_and_prox()
         self.current_solver_options = self.iterk_solver_options
         return self.trivial_bound
+
+    ITER0_CONTINUATIONS = 3
+
+    def _iter0_continue(self, dtiming, verbose):
+        """Iter0 LPs left at the PDHG iteration cap on the streaming path (path 4: large
+        scenarios sharing one matrix, config 5) are continued, not accepted: a warm re-solve
+        of every local scenario (the converged ones stop at their first KKT check) in which
+        the longest ones -- those at the cap -- run first, each over the whole GPU (the split
+        form, phgpu_options.split_longest), up to ITER0_CONTINUATIONS times.  The reference
+        takes Iter0's x and Lower_bound from a solver that finished (spopt.py:175-206); a
+        larger iteration cap on the queue would leave the stragglers in one slot each.
+        Returns the continuation solves run."""
+        n = 0
+        if not self.engine.shared or self.options.get("iter0_continue", True) is False:
+            return 0
+        while n < self.ITER0_CONTINUATIONS:
+            st = self.engine.host("status")
+            lim = int((st == _lib.ITER_LIMIT).sum())
+            if lim == 0:
+                break
+            opts = dict(self.current_solver_options)
+            opts["split_longest"] = min(16, lim)
+            self.solve_loop(solver_options=opts, dtiming=dtiming, gripe=False, verbose=verbose, warm_start=True)
+            n += 1
+        return n
 
     # phbase.py:875-979
     def _speculate(self, have_ext):

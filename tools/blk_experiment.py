@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--S", type=int, default=1024)
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--lanes", type=int, default=64, help="threads per scenario (64 WPS)")
     ap.add_argument("--sub", type=int, default=0, help="solve only every k-th scenario (x̄ from the oracle)")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--tmpl", default=None)
@@ -38,7 +39,7 @@ def main():
     from oracle import farmer_vec as fv
     names = farmer.scenario_names_creator(a.S)
     b = farmer.batch_creator(names, crops_multiplier=a.cm, num_scens=a.S)
-    src, _ = L.ipm_source(b, 64)
+    src, _ = L.ipm_source(b, a.lanes)
     if a.tmpl:
         tmpl = open(a.tmpl).read()
         k = src.index("// jit_ipm_blk.hip.in --")
@@ -65,7 +66,7 @@ def main():
     try:
         t0 = time.time()
         st8 = []
-        x, y, obj, bound, st, it = ipm_wave_host.solve(bs, eps_rel=1e-10, stats=st8)
+        x, y, obj, bound, st, it = ipm_wave_host.solve(bs, lanes=a.lanes, eps_rel=1e-10, stats=st8)
         print(f"iter0 ({S} scenarios) {time.time() - t0:.1f}s mean {it[st == 0].mean():.2f} max {it.max()} "
               f"fail {(st != 0).sum()}", flush=True)
         allit = []
@@ -75,7 +76,8 @@ def main():
             st8 = []
             t0 = time.time()
             xprev, yprev = x, y
-            x, y, obj, bound, st, it = ipm_wave_host.solve(bs, W=W, rho=rho, xbar=xbar, x_in=x, y_in=y, stats=st8)
+            x, y, obj, bound, st, it = ipm_wave_host.solve(bs, lanes=a.lanes, W=W, rho=rho, xbar=xbar, x_in=x, y_in=y,
+                                                           stats=st8)
             xv = oph.x[sub]
             ok = st == 0
             err = np.abs(x[:, nc] - xv).max(1)
@@ -91,7 +93,7 @@ def main():
                 L.ipm_source = lambda batch, lanes=1: (tsrc, None)  # noqa: E731
                 one = farmer.batch_creator([names[sub[i]]], crops_multiplier=a.cm, num_scens=a.S)
                 print("trace of", names[sub[i]], "iterations", int(it[i]), flush=True)
-                ipm_wave_host.solve(one, W=W[i:i + 1], rho=rho[i:i + 1], xbar=xbar[i:i + 1], x_in=xprev[i:i + 1],
+                ipm_wave_host.solve(one, lanes=a.lanes, W=W[i:i + 1], rho=rho[i:i + 1], xbar=xbar[i:i + 1], x_in=xprev[i:i + 1],
                                     y_in=yprev[i:i + 1])
                 L.ipm_source = lambda batch, lanes=1: (src, None)  # noqa: E731
             # a scenario left to the fallback continues from the oracle's solution (the PDHG's)
