@@ -174,7 +174,7 @@ def _spawn(case, tmp_path):
 def _assert_multirank_step(rec, iters, lanes):
     """Path 6 on its expected lane count, every PH step through reduce -> all-reduce ->
     update_ex with the conv all-reduce on the side stream, nothing folded or fused."""
-    assert rec["path"] == 6 and rec["compiled"] == 1 and rec["scratch"] == 0, rec
+    assert rec["path"] == 6 and rec["compiled"] == 1 and rec["scratch"] <= 1024, rec
     assert rec["lanes"] == lanes, rec
     c = rec["calls"]
     assert c["ph_reduce"] >= iters and c["allreduce_xbar"] == c["ph_reduce"], c
@@ -235,9 +235,8 @@ def test_two_rank_aircond65536_node_reductions(gpu, tmp_path):
         assert r[k]["spec"]
         assert abs(r[k]["tb"] - g["trivial_bound"]) <= OBJ_REL * abs(g["trivial_bound"]), (k, r[k]["tb"])
         rec = r[k]["rec"]
-        # aircond's one-lane module spills: lane groups of 4 above 8,192 local scenarios
-        _assert_multirank_step(rec, g["ph_iters"], lanes=rec["lanes"])
-        assert rec["lanes"] in (1, 4), rec
+        # one lane above 16,384 local scenarios (aircond's module spills 524 B per lane)
+        _assert_multirank_step(rec, g["ph_iters"], lanes=1)
         assert r[k]["all_optimal"]
         conv = np.array(r[k]["conv"])
         assert np.abs(conv - np.array(g["conv"])).max() <= ABS, (k, conv, g["conv"])

@@ -313,11 +313,12 @@ def test_lane_groups_hand_infeasible_scenarios_to_the_pdhg(gpu, ipm_lanes, kind,
 
 
 @pytest.mark.parametrize("model,S,lanes", [("farmer", 8192, 8), ("farmer", 16384, 4), ("farmer", 32768, 1),
-                                           ("aircond", 16384, 4)])
+                                           ("aircond", 16384, 4), ("aircond", 32768, 1)])
 def test_lane_policy_by_share(gpu, model, S, lanes):
     """ipm_lanes (solve_ipm.inc): lane groups of 8 for <= 8,192 local scenarios, of 4 for
-    <= 16,384 and for a pattern whose one-lane module spills (aircond), one lane above --
-    and the automatic solve stays on path 6 without scratch."""
+    <= 16,384, one lane above -- also for aircond, whose one-lane module spills 524 B per
+    lane (below IPM_SPILL_MAX: 0.315 ms per solve at 65,536 against 0.426 on lane groups of
+    4); the lane-group modules stay scratch-free."""
     from mpisppy_amd import _lib
     from mpisppy_amd.engine import PHEngine
     from mpisppy_amd.examples import aircond, farmer
@@ -326,11 +327,12 @@ def test_lane_policy_by_share(gpu, model, S, lanes):
     else:
         kw = {"Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50, "mu_dev": 0, "sigma_dev": 40,
               "start_seed": 0}
-        b = aircond.batch_creator(aircond.scenario_names_creator(S), branching_factors=[8, 32, 64], **kw)
+        b = aircond.batch_creator(aircond.scenario_names_creator(S), branching_factors=[S // 2048, 32, 64], **kw)
     e = PHEngine(b, device="cuda:0")
     e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
     ii = e.ipm_info()
-    assert e.kernel_info()["path"] == 6 and ii["lanes"] == lanes and ii["scratch_bytes"] == 0, ii
+    assert e.kernel_info()["path"] == 6 and ii["lanes"] == lanes and ii["off"] == 0, ii
+    assert ii["scratch_bytes"] == 0 if (lanes > 1 or model == "farmer") else 0 < ii["scratch_bytes"] <= 1024, ii
     assert (e.host("status") == 0).all()
     e.close()
 
