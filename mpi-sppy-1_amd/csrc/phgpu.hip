@@ -1145,7 +1145,15 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
         double t = 0.0;
         for (int u = 0; u < nwb; ++u) t += red[u];
         const double old = __hip_atomic_exchange(&o.cpart[bid], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("" ::"v"(old) : "memory");  // the swap has returned before the ticket
+        // The swap has returned before the ticket is taken (the empty asm consumes its result,
+        // so the compiler waits for it).  Ordering rests on the hardware, not on the HIP memory
+        // model (both RMWs are relaxed): a returning agent-scope atomic has been performed at
+        // the device's coherence point when its value is back, so the last block's reads of
+        // cpart (agent-scope RMWs as well) see every partial whose ticket precedes its own.
+        // Release / acquire would make it formal at the price of an L2 writeback on every XCD
+        // (15-29 us per launch).  tests/test_gpu_readback.py compares this conv
+        // bit for bit with the ordered device reduction and would catch a reordering.
+        asm volatile("" ::"v"(old) : "memory");
         const int tk = __hip_atomic_fetch_add(o.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = tk == nblk - 1;
     }

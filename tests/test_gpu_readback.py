@@ -79,6 +79,12 @@ def test_update_ex_host_conv_and_stats(gpu, kernel):
                                      e.W.data_ptr(), e.rho.data_ptr(), 1, e.conv_buf.data_ptr(), e._stream()),
                "phgpu_ph_update")
     conv_dev = float(e.conv_buf.item())
+    # the last-block reduction (a hardware ordering of relaxed atomics, phgpu.hip
+    # conv_last_block) against an independent sum: a block partial read before its swap landed
+    # would be off by a whole block's share (phbase.py:321-343: mean |x - x̄| over nonants)
+    nc = torch.as_tensor(e.batch.nonant_col, dtype=torch.long, device=e.device)
+    ref = (e.x.index_select(0, nc) - e.xbar[:e.nn]).abs().sum().item() / (e.S * e.nn)
+    assert abs(conv_dev - ref) <= 1e-12 * abs(ref), (conv_dev, ref)
     ref_stats = torch.zeros(6, dtype=torch.int64).pin_memory()
     _lib.check(e.lib.phgpu_solve_stats(e.h, ref_stats.data_ptr(), e._stream()), "phgpu_solve_stats")
     torch.cuda.synchronize()
