@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--rho", type=float, default=1.0)
     p.add_argument("--eps", type=float, default=None,
                    help="PDHG eps_rel of the PH solves (default 1e-9; uc: 1e-6 for Iter0 and PH)")
+    p.add_argument("--no-conv-overlap", action="store_true",
+                   help="N > 1: the conv all-reduce on the launch stream ahead of the next solve "
+                        "instead of on a side stream under it (the comparison for the overlap)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                    help="torch.distributed backend for N > 1 (auto: RCCL when every rank has its own GPU)")
     p.add_argument("--solver-opt", action="append", default=[], metavar="KEY=VALUE",
@@ -521,6 +524,7 @@ def main():
     log(f"[bench] model built ({time.perf_counter() - t_setup:.1f} s)")
     with contextlib.redirect_stdout(sys.stderr):
         ph.PH_Prep()
+        ph.engine.overlap_conv = not a.no_conv_overlap
         log(f"[bench] PH_Prep done ({time.perf_counter() - t_setup:.1f} s)")
         trivial_bound = ph.Iter0()
         log(f"[bench] Iter0 done ({time.perf_counter() - t_setup:.1f} s)")
@@ -604,6 +608,8 @@ def main():
                                                 if k != "eps_rel"},
                        "scenarios_per_gpu": b.S,
                        "n": b.n, "m": b.m, "nnz": b.nnz,
+                       "conv_allreduce": (("launch stream, ahead of the next solve" if a.no_conv_overlap
+                                           else "side stream, under the next solve") if world > 1 else None),
                        "parallelism": (f"scenario-sharded x{world}" +
                                        (f" ({'RCCL' if backend == 'nccl' else 'gloo, ranks sharing a GPU'}"
                                         f" x̄ all-reduce)" if world > 1 else ""))},

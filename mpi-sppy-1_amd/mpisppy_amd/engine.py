@@ -122,7 +122,10 @@ class PHEngine:
         _track(self)
         # library calls of the PH step, by kind (tests assert which path a loop took)
         self.calls = {"ph_reduce": 0, "ph_update_ex": 0, "ph_step_local": 0, "ph_step_defer": 0,
-                      "allreduce_xbar": 0, "allreduce_conv_side": 0}
+                      "allreduce_xbar": 0, "allreduce_conv_side": 0, "allreduce_conv_main": 0}
+        # several ranks: the conv all-reduce on a side stream under the next solve (False: on
+        # the launch stream ahead of it -- bench.py --no-conv-overlap, the comparison case)
+        self.overlap_conv = True
         dev = self.device
         self.A_val = _dev_T(b.A_val[0] if self.shared else b.A_val, dev)
         self.c = _dev_T(b.c, dev)
@@ -539,6 +542,17 @@ class PHEngine:
         if self._conv_zero_copy:
             return
         main = torch.cuda.current_stream(self.device)
+        if self._conv_ev is None:
+            self._conv_ev = torch.cuda.Event()
+        if not self.overlap_conv:
+            # (the comparison case of the bench: the conv all-reduce ahead of the next solve on
+            # the launch stream, as the reference's Allreduce sits in the loop)
+            self.calls["allreduce_conv_main"] += 1
+            self._allreduce_sum_(self.conv_buf, tag="critical")
+            self._conv_host.copy_(self.conv_buf, non_blocking=True)
+            self._conv_ev.record(main)
+            self._upd_marks[self._upd_seq] = self._conv_ev
+            return
         ev = torch.cuda.Event()
         ev.record(main)
         self._upd_marks[self._upd_seq] = ev        # (also the update's marker for its stats)
@@ -553,8 +567,6 @@ class PHEngine:
             # write the 8 bytes piecewise, and a poll caught a half-written value (its top
             # byte still the NaN sentinel's: 9.4e306 as conv on one rank, round-5 2-rank
             # test), which could make ranks disagree on the break and deadlock
-            if self._conv_ev is None:
-                self._conv_ev = torch.cuda.Event()
             self._conv_ev.record(self._side)
 
     _SPIN = 200000

@@ -13,20 +13,4 @@ step smoke 200 python3 -u -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python3 -u bench.py
 step prof3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof3 -o run -- python3 -u bench.py --no-cpu-baseline
 step prof2 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof2 -o run -- python3 -u bench.py --no-cpu-baseline --scens 1024 --cm 10
-P="python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline"
-for cfg in c3 c2 c4 s8192; do
-  case $cfg in c3) C="$P";; c2) C="$P --scens 1024 --cm 10";; c4) C="$P --model aircond";; s8192) C="$P --scens 8192";; esac
-  step pmcf_$cfg 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcf_$cfg -o run -- $C
-  step pmcw_$cfg 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_$cfg -o run -- $C
-  step sqa_$cfg 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_WAVES SQ_WAVE_CYCLES --output-format csv -d $O/sqa_$cfg -o run -- $C
-  step sqb_$cfg 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_ANY --output-format csv -d $O/sqb_$cfg -o run -- $C
-done
-B="python3 -u bench.py --no-cpu-baseline"
-step b_cfg2 300 $B --scens 1024 --cm 10
-step b_cfg4 300 $B --model aircond
-step b_s32768 200 $B --scens 32768
-step b_s16384 200 $B --scens 16384
-step b_s8192 200 $B --scens 8192
-step b_cm64 400 $B --cm 64 --steps 10 --warmup 3
-step b_gloo2 300 $B --gpus 2 --backend gloo
 echo done
