@@ -155,6 +155,14 @@ int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
                         const double* prob, const int32_t* node_of,
                         const double* prob_coeff, void* stream);
 
+/* Variable probabilities (spbase.py:394-424, phbase.py:54-79 and 315-318): pvar, device
+ * [nn*S] (k-major like W), the probability coefficient of nonant k of scenario s in the x̄
+ * sums in place of the per-node prob_coeff; Update_W then sets W[k,s] = 0 where pvar[k,s]
+ * is 0 (prob0_mask).  Read at every reduce / update (not copied); NULL restores the per-node
+ * coefficients.  While set, the PH step always runs as phgpu_ph_reduce + phgpu_ph_update
+ * (no epilogue partials, no folded or fused step). */
+int phgpu_set_nonant_probs(phgpu_handle h, const double* pvar);
+
 /* Bind the PH objective terms for the next solves (phbase.py:585-699):
  *   objective = f(x) + W_on * sum_k W[k,s] x_k + prox_on * sum_k rho[k,s]/2 (x_k - xbar[k,s])^2
  * W, rho, xbar: device [nn*S]; they are read at solve time (not copied). */

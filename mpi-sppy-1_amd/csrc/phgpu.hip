@@ -66,6 +66,9 @@ struct phgpu_state {
     int32_t *nonant_col, *nonant_depth, *nonant_off, *nonant_slot;
     // per-scenario problem data (library copies)
     double *A, *c, *lb, *ub, *rl, *ru, *q, *objc, *prob, *pcoef;
+    // per-nonant probability coefficients ([nn][S], caller-owned; null: the per-node pcoef),
+    // the variable probabilities of spbase.py:394-424 (phgpu_set_nonant_probs)
+    const double* pvar;
     int32_t* node_of;
     // scaling
     double *Ah_csr, *Ah_csc, *Dr, *Dc, *normA;
@@ -936,7 +939,7 @@ k_xbar_partial(phgpu_state st, const double* __restrict__ x, double* __restrict_
         const int k = blockIdx.y;
         const int d = st.nonant_depth[k];
         const int gnode = act ? st.node_of[IX(d)] : -1;
-        const double w = act ? st.pcoef[IX(d)] : 0.0;
+        const double w = act ? (st.pvar ? st.pvar[IX(k)] : st.pcoef[IX(d)]) : 0.0;
         const double v = act ? x[IX(st.nonant_col[k])] : 0.0;
         const int g0 = __shfl(gnode, 0, WAVE);
         const bool uniform = !__any(act && gnode != g0);
@@ -992,7 +995,7 @@ __device__ __forceinline__ void xp_recompute(const phgpu_state& st, const double
     const int64_t s1 = (w + 1) * C < S ? (w + 1) * C : S;
     a = b = 0.0;
     for (int64_t s = w * C; s < s1; ++s) {
-        const double p = st.pcoef[IX(d)], v = x[IX(j)];
+        const double p = st.pvar ? st.pvar[IX(k)] : st.pcoef[IX(d)], v = x[IX(j)];
         a += p * v;
         b += p * v * v;
     }
@@ -1198,7 +1201,8 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
         const double xb = node_buf[gnode * st.nlen_max + st.nonant_off[k]];
         const double xv = x[IX(st.nonant_col[k])];
         xbar[IX(k)] = xb;
-        if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
+        // (variable probabilities: W masked where the probability is 0, phbase.py:315-318)
+        if (update_W) W[IX(k)] = (st.pvar && st.pvar[IX(k)] == 0.0) ? 0.0 : W[IX(k)] + rho[IX(k)] * (xv - xb);
         acc += fabs(xv - xb);
     }
     conv_last_block(acc, o);
@@ -2335,6 +2339,13 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     return 0;
 }
 
+extern "C" int phgpu_set_nonant_probs(phgpu_handle h, const double* pvar) {
+    FLUSH_STEP(h);
+    if (!h) return set_err(-1, "null handle");
+    h->pvar = h->nn > 0 ? pvar : nullptr;
+    return 0;
+}
+
 extern "C" int phgpu_set_ph_state(phgpu_handle h, const double* W, const double* rho,
                                   const double* xbar, int W_on, int prox_on) {
     FLUSH_STEP(h);
@@ -2943,6 +2954,12 @@ extern "C" int phgpu_ph_step_local(phgpu_handle h, const double* x, double* node
         return set_err(-1, "null argument");
     if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_step_local: stats_out before any solve");
     FLUSH_STEP(h);
+    if (h->pvar) {
+        // variable probabilities: the generic reduce + update (per-nonant weights, W mask)
+        const int rc = phgpu_ph_reduce(h, x, node_buf, stream);
+        if (rc) return rc;
+        return phgpu_ph_update_ex(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, stream);
+    }
     return step_local_impl(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, (hipStream_t)stream);
 }
 
@@ -2953,6 +2970,8 @@ extern "C" int phgpu_ph_step_defer(phgpu_handle h, const double* x, double* node
         return set_err(-1, "null argument");
     if (stats_out && !h->last_status) return set_err(-1, "phgpu_ph_step_defer: stats_out before any solve");
     FLUSH_STEP(h);
+    // (variable probabilities: no folded step, the step runs now)
+    if (h->pvar) return phgpu_ph_step_local(h, x, node_buf, xbar, W, rho, update_W, conv_local, stats_out, stream);
     phgpu_state::ph_pending& q = h->pend;
     q.active = 1;
     q.x = x;

@@ -153,6 +153,7 @@ class PHEngine:
         self.conv_buf = z(1)
         self.exp_buf = z(5)
         self.xfix = None
+        self.pvar = None          # per-nonant probability coefficients (set_nonant_probs)
         self.W_on = 0
         self.prox_on = 0
         # row duals are an optional phgpu_solve output: PH never reads them, so the hot
@@ -253,6 +254,18 @@ class PHEngine:
     def set_W(self, W):
         self._flush_step()
         self.W.copy_(_dev_T(np.asarray(W, dtype=np.float64), self.device))
+
+    def set_nonant_probs(self, var_prob):
+        """Per-nonant probability coefficients, host [S, nn] (SPBase.var_prob), or None:
+        the x̄ weights and the Update_W mask of variable probabilities (phgpu_set_nonant_probs,
+        spbase.py:394-437, phbase.py:315-318)."""
+        self._flush_step()
+        if var_prob is None:
+            self.pvar = None
+        else:
+            self.pvar = _dev_T(np.asarray(var_prob, dtype=np.float64), self.device)
+            assert tuple(self.pvar.shape) == (self.nn, self.S), self.pvar.shape
+        _lib.check(self.lib.phgpu_set_nonant_probs(self.h, _ptr(self.pvar)), "phgpu_set_nonant_probs")
 
     def set_xbar(self, xbar):
         self._flush_step()

@@ -42,8 +42,7 @@ class SPBase:
             self.all_nodenames = list(all_nodenames)
         else:
             raise RuntimeError("'ROOT' must be in the list of node names")
-        if variable_probability is not None:
-            raise NotImplementedError("variable_probability is outside the batched PH hot path")
+        self.variable_probability = variable_probability
         self.multistage = len(self.all_nodenames) > 1
         self.mpicomm = mpicomm if mpicomm is not None else Comm()
         self.cylinder_rank = self.mpicomm.Get_rank()
@@ -63,6 +62,7 @@ class SPBase:
         self.node_names = nonleaf_nodenames(self.all_nodenames)
         self.scenario_creator_kwargs = scenario_creator_kwargs or {}
         self._create_scenarios()
+        self._use_variable_probability_setter()
 
     def _create_scenarios(self):
         kw = self.scenario_creator_kwargs
@@ -100,3 +100,74 @@ class SPBase:
         missing = [o for o in required_options if o not in given_options]
         if missing:
             raise ValueError(f"Missing option(s) {missing}")
+
+    # spbase.py:394-437
+    def _use_variable_probability_setter(self, verbose=False):
+        """Per-nonant probability coefficients (``variable_probability(model, **kwargs)`` ->
+        [(id(vardata), prob)]; spbase.py:394-437): ``self.var_prob`` [S_local, nn], each
+        nonant's node coefficient (prob_coeff) unless the function names it, and
+        ``self.prob0_mask`` (prob != 0) -- the x̄ weights of _Compute_Xbar and the W mask of
+        Update_W (phbase.py:54-79, 315-318), on the device through phgpu_set_nonant_probs.
+        With a batch_creator there are no per-scenario models: pass the [S_local, nn] array
+        as ``options["variable_probability_array"]``."""
+        self.var_prob = None
+        self.prob0_mask = None
+        arr = self.options.get("variable_probability_array")
+        if self.variable_probability is None and arr is None:
+            return
+        b = self.batch
+        dep = np.asarray(b.nonant_depth, dtype=np.int64)
+        vp = np.asarray(b.prob_coeff, dtype=np.float64)[:, dep].copy()
+        if arr is not None:
+            arr = np.asarray(arr, dtype=np.float64)
+            if arr.shape != vp.shape:
+                raise ValueError(f"variable_probability_array has shape {arr.shape}, expected {vp.shape}")
+            vp[:] = arr
+        else:
+            if not self.local_scenarios:
+                raise RuntimeError("variable_probability needs per-scenario models; with a batch_creator pass "
+                                   "options['variable_probability_array']")
+            kw = self.options.get("variable_probability_kwargs", {})
+            for s, nm in enumerate(self.local_scenario_names):
+                mdl = self.local_scenarios[nm]
+                id2k = {}
+                k = 0
+                for nd in mdl._mpisppy_node_list:
+                    for v in nd.nonant_vardata_list:
+                        id2k[id(v)] = k
+                        k += 1
+                for vid, prob in self.variable_probability(mdl, **kw):
+                    vp[s, id2k[vid]] = prob
+        self.var_prob = vp
+        self.prob0_mask = (vp != 0.0).astype(np.float64)
+        if not self.options.get("do_not_check_variable_probabilities", False):
+            self._check_variable_probabilities_sum(verbose)
+
+    # spbase.py:456-497
+    def _check_variable_probabilities_sum(self, verbose=False):
+        """Every nonant's coefficients sum to 1 over its node's scenarios (all ranks)."""
+        import torch
+        b = self.batch
+        gid = {nd: i for i, nd in enumerate(self.node_names)}
+        node_of = np.array([[gid[b.node_names[g]] for g in row] for row in np.asarray(b.node_of)], dtype=np.int64)
+        nl = max(1, int(b.nlen_max))
+        acc = np.zeros((len(self.node_names), nl))
+        seen = np.zeros((len(self.node_names), nl))
+        dep = np.asarray(b.nonant_depth, dtype=np.int64)
+        off = np.asarray(b.nonant_off, dtype=np.int64)
+        for k in range(b.nn):
+            np.add.at(acc, (node_of[:, dep[k]], off[k]), self.var_prob[:, k])
+            seen[node_of[:, dep[k]], off[k]] = 1.0
+        t = torch.from_numpy(np.concatenate([acc.ravel(), seen.ravel()]))
+        import torch.distributed as dist
+        if self.n_proc > 1 and dist.get_backend() == "nccl":
+            t = t.cuda()                      # (RCCL reduces device tensors only)
+        self.mpicomm.allreduce_sum_(t)
+        t = t.cpu()
+        acc = t[:acc.size].numpy().reshape(acc.shape)
+        seen = t[acc.size:].numpy().reshape(acc.shape) > 0
+        bad = seen & ~np.isclose(acc, 1.0, atol=self.E1_tolerance)
+        if bad.any():
+            g, i = np.argwhere(bad)[0]
+            raise RuntimeError(f"Node {self.node_names[g]}, nonant {i} has conditional probability sum {acc[g, i]}")
+

@@ -48,6 +48,8 @@ class SPOpt(SPBase):
         if self.engine is None:
             self.engine = PHEngine(self.batch, device=self.options.get("device"), comm=self.mpicomm,
                                    node_names=self.node_names, shared=self.options.get("shared_matrix"))
+            if getattr(self, "var_prob", None) is not None:
+                self.engine.set_nonant_probs(self.var_prob)
 
     # options the reference's cfg_vanilla.shared_options passes to MIP/LP plugins
     # (threads, mipgap; cfg_vanilla.py:41-62) or that only drive plugin output (Tee):

@@ -30,7 +30,7 @@ class OraclePH:
     """Single-process restatement of PH over a list of oracle ScenLP scenarios."""
 
     def __init__(self, scens, default_rho, n_proc=1, rho_setter=None, solver="ipm",
-                 farmer_info=None):
+                 farmer_info=None, var_prob=None):
         self.scens = scens
         S = len(scens)
         for s in scens:
@@ -58,6 +58,9 @@ class OraclePH:
                 off += len(idx)
             self.node_slices.append(sl)
             self.prob_coeff.append(pc)
+        # variable probabilities (spbase.py:394-437): per-nonant coefficients [S, nn] replacing
+        # the node's prob_coeff in the x̄ sums, and W masked where they are 0 (phbase.py:315-318)
+        self.var_prob = None if var_prob is None else np.asarray(var_prob, dtype=np.float64)
         self.rho = np.full((S, self.nn), float(default_rho))
         self.rho_setter = rho_setter
         self.W = np.zeros((S, self.nn))
@@ -110,6 +113,8 @@ class OraclePH:
         for k in range(len(self.scens)):
             for (ndn, a, b), pc in zip(self.node_slices[k], self.prob_coeff[k]):
                 xs = self.x[k, a:b]
+                if self.var_prob is not None:
+                    pc = self.var_prob[k, a:b]
                 if ndn not in acc:
                     acc[ndn] = [np.zeros(b - a), np.zeros(b - a)]
                 acc[ndn][0] += pc * xs
@@ -123,6 +128,8 @@ class OraclePH:
     # -- phbase.py:293-318
     def update_W(self):
         self.W += self.rho * (self.x - self.xbar)
+        if self.var_prob is not None:
+            self.W *= (self.var_prob != 0.0)                       # prob0_mask
 
     # -- phbase.py:321-343
     def convergence_diff(self):
