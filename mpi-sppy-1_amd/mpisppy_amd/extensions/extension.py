@@ -1,9 +1,14 @@
 """Extension hooks of the PH loop (mirrors mpisppy/extensions/extension.py:12-170).
 
 The hook points and their place in the loop are the reference's (phbase.py Iter0 /
-iterk_loop / post_loops; spopt.py solve_loop).  ``pre_solve`` / ``post_solve`` are kept
-for API compatibility but never fire: one batched device solve replaces the
-per-scenario ``solve_one`` calls they bracket in the reference (spopt.py:85-223).
+iterk_loop / post_loops; spopt.py solve_loop).  The per-scenario ``pre_solve`` /
+``post_solve`` bracket the one batched device solve that replaces the reference's
+``solve_one`` calls (spopt.py:146-147, 220-221): every local scenario's ``pre_solve`` runs
+before the launch, every ``post_solve`` after it, with the scenario's solution loaded and a
+results object per scenario (``spopt.ScenarioResults``; None for an infeasible or unbounded
+one, as the reference passes).  A hook that edits a scenario's model does not change the
+batched solve (its data are on the device); ``overrides`` tells which hooks an extension
+defines, so the others cost nothing.
 """
 
 
@@ -79,3 +84,17 @@ def _fan_out(name):
 
 for _h in _HOOKS:
     setattr(MultiExtension, _h, _fan_out(_h))
+
+
+def overrides(ext, name):
+    """True if ``ext`` defines hook ``name`` beyond the base class's no-op (for a
+    MultiExtension: if any member does).  The PH loop skips, or keeps its speculative
+    solve around, hooks that do nothing."""
+    if ext is None:
+        return False
+    if isinstance(ext, MultiExtension):
+        return any(overrides(e, name) for e in ext.extdict.values())
+    f = getattr(type(ext), name, None)
+    if f is None:
+        return callable(getattr(ext, name, None))
+    return f is not getattr(Extension, name, None)

@@ -13,6 +13,7 @@ import numpy as np
 
 from . import _lib, global_toc
 from .spopt import SPOpt
+from .extensions.extension import overrides
 
 
 LP_EPS_REL = 1e-10
@@ -269,8 +270,8 @@ class PHBase(SPOpt):
             # path 4 keeps one warm-start slot (phgpu_solve_deferred is rejected), and its
             # solves take seconds, against the ~0.05 ms a speculative launch hides
             return False
-        if have_ext and any(hasattr(self.extobject, h) for h in ("miditer", "pre_solve_loop", "post_solve_loop",
-                                                                  "pre_solve", "post_solve")):
+        if have_ext and any(overrides(self.extobject, h) for h in ("miditer", "pre_solve_loop", "post_solve_loop",
+                                                                    "pre_solve", "post_solve")):
             return False
         return True
 

@@ -7,8 +7,9 @@ per-scenario ``solve_one`` + SolverFactory plugin call (spopt.py:85-223) with ON
 (aliases below).  ``iter0_solver_options`` / ``iterk_solver_options`` keys are the
 fields of ``phgpu_options`` (include/phgpu.h).
 
-Documented limitation: per-scenario extension hooks ``pre_solve`` / ``post_solve``
-cannot run inside a batched solve; ``pre_solve_loop`` / ``post_solve_loop`` do.
+Per-scenario extension hooks ``pre_solve`` / ``post_solve`` (spopt.py:146-147, 220-221)
+bracket the batched solve: all local scenarios' ``pre_solve`` before the launch, all
+``post_solve`` after it (solutions loaded, one ``ScenarioResults`` each).
 """
 import time
 import numpy as np
@@ -16,6 +17,50 @@ import numpy as np
 from . import _lib
 from .spbase import SPBase
 from .engine import PHEngine
+from .extensions.extension import overrides
+
+_TERMINATION = {_lib.OPTIMAL: "optimal", _lib.ITER_LIMIT: "maxIterations",
+                _lib.PRIMAL_INFEASIBLE: "infeasible", _lib.DUAL_INFEASIBLE: "unbounded"}
+
+
+class ScenarioResults:
+    """What ``post_solve`` gets for one scenario, in the shape of the Pyomo results the
+    reference passes (spopt.py:165-206): ``solver.termination_condition`` /
+    ``solver.status``, ``Problem[0].Lower_bound`` / ``Upper_bound`` (the Lagrangian bound
+    and the objective of the solve, swapped for a maximisation), plus the engine's own
+    ``status`` code and ``iterations``."""
+
+    class _Solver:
+        def __init__(self, tc):
+            self.termination_condition = tc
+            self.status = "ok" if tc in ("optimal", "maxIterations") else "warning"
+
+    class _Problem:
+        def __init__(self, lo, up):
+            self.Lower_bound = lo
+            self.Upper_bound = up
+
+    def __init__(self, status, obj, bound, iterations, sense=1):
+        self.status = int(status)
+        self.iterations = int(iterations)
+        self.solver = self._Solver(_TERMINATION.get(self.status, "error"))
+        lo, up = (bound, obj) if sense > 0 else (obj, bound)
+        self.Problem = [self._Problem(float(lo), float(up))]
+        self.solution = [self] if self.status in (_lib.OPTIMAL, _lib.ITER_LIMIT) else []
+
+
+class ScenarioView:
+    """The subproblem handed to ``pre_solve`` / ``post_solve`` when the scenarios were
+    built by a ``batch_creator`` (no per-scenario models): its name, its index in the local
+    batch and, after the solve, its x."""
+
+    def __init__(self, opt, k, name):
+        self._opt, self.index, self.name = opt, k, name
+        self._name = name
+
+    @property
+    def x(self):
+        return self._opt.engine.host("x")[self.index]
 
 SOLVER_NAMES = ("mi355x_pdhg", "phgpu", "mi355x")
 
@@ -71,6 +116,11 @@ class SPOpt(SPBase):
                    warm_start=True, speculative=False):
         if self.extensions is not None and hasattr(self.extobject, "pre_solve_loop"):
             self.extobject.pre_solve_loop()
+        ext = self.extobject if self.extensions is not None else None
+        pre, post = overrides(ext, "pre_solve"), overrides(ext, "post_solve")
+        if pre:
+            for sp in self._subproblems():
+                ext.pre_solve(sp)
         t0 = time.perf_counter()
         self.engine.solve(self._to_phgpu_options(solver_options), warm=warm_start, speculative=speculative)
         if dtiming or self.options.get("record_pdhg_iters", False):
@@ -79,6 +129,8 @@ class SPOpt(SPBase):
             it = self.engine.iters.cpu().numpy()
             self.pdhg_iters.append((int(it.max()), float(it.mean())))
         self.solve_times.append(time.perf_counter() - t0)
+        if post:
+            self._post_solve_hooks(ext)
         if self.extensions is not None and hasattr(self.extobject, "post_solve_loop"):
             self.extobject.post_solve_loop()
         if dtiming and self.cylinder_rank == 0:
@@ -91,6 +143,22 @@ class SPOpt(SPBase):
             self._gripe_pending = True
         elif gripe and self.engine.count_not_optimal() > 0:
             self._gripe_print()
+
+    def _subproblems(self):
+        """Per-scenario models when the creator built them, else ScenarioViews."""
+        if self.local_scenarios:
+            return [self.local_scenarios[nm] for nm in self.local_scenario_names]
+        return [ScenarioView(self, k, nm) for k, nm in enumerate(self.local_scenario_names)]
+
+    def _post_solve_hooks(self, ext):
+        # (a speculative solve is never bracketed: PHBase._speculate is off with these hooks)
+        self.load_solutions_to_models()
+        st, obj, bd, it = (self.engine.host(k) for k in ("status", "obj", "bound", "iters"))
+        sense = self.batch.sense
+        for k, sp in enumerate(self._subproblems()):
+            failed = st[k] in (_lib.PRIMAL_INFEASIBLE, _lib.DUAL_INFEASIBLE)
+            res = None if failed else ScenarioResults(st[k], sense * obj[k], sense * bd[k], it[k], sense)
+            ext.post_solve(sp, res)
 
     def gripe_report(self):
         """The gripe of a solve_loop(gripe="deferred") (spopt.py:284-294 prints it right
