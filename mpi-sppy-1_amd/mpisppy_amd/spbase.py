@@ -161,7 +161,7 @@ class SPBase:
         t = torch.from_numpy(np.concatenate([acc.ravel(), seen.ravel()]))
         import torch.distributed as dist
         if self.n_proc > 1 and dist.get_backend() == "nccl":
-            t = t.cuda()                      # (RCCL reduces device tensors only)
+            t = t.to(self.options.get("device") or "cuda")  # (RCCL reduces device tensors only)
         self.mpicomm.allreduce_sum_(t)
         t = t.cpu()
         acc = t[:acc.size].numpy().reshape(acc.shape)
