@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--tmpl", default=None)
     ap.add_argument("--save", default=None)
     ap.add_argument("--trace", type=int, default=0, help="trace the slowest scenario of this PH iteration")
+    ap.add_argument("--cold", action="store_true", help="every PH solve starts cold (no x_in / y_in)")
     a = ap.parse_args()
     import ipm_wave_host
     import mpisppy_amd._lib as L
@@ -76,7 +77,8 @@ def main():
             st8 = []
             t0 = time.time()
             xprev, yprev = x, y
-            x, y, obj, bound, st, it = ipm_wave_host.solve(bs, lanes=a.lanes, W=W, rho=rho, xbar=xbar, x_in=x, y_in=y,
+            x, y, obj, bound, st, it = ipm_wave_host.solve(bs, lanes=a.lanes, W=W, rho=rho, xbar=xbar,
+                                                           x_in=None if a.cold else x, y_in=None if a.cold else y,
                                                            stats=st8)
             xv = oph.x[sub]
             ok = st == 0
