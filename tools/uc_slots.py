@@ -5,7 +5,7 @@ list-scheduling study of how many resident slots pay).
     python tools/uc_slots.py '<json list of {"PER_CU": k, "SPLIT": T, "SLOTS": B}>'
 
 Iter0 is a cold solve (cap 100,000) and one warm continuation solve; PH iteration k then
-runs with layout k mod len(list).  Writes gpurun_out/uc_slots.npz (iters [K, S], times)."""
+runs with layout k mod len(list).  Writes gpurun_out/uc_slots.npz (iters [K, S], times).  UC_K: PH iterations (default: one per layout)."""
 import json
 import os
 import sys
@@ -26,7 +26,7 @@ e = PHEngine(b, device="cuda:0")
 
 
 def env(lay):
-    for k in ("PER_CU", "SPLIT", "SLOTS"):
+    for k in ("PER_CU", "SPLIT", "SLOTS", "PAIR"):
         v = lay.get(k)
         name = "PHGPU_STREAM_" + k
         if v is None:
