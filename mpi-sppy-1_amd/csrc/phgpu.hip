@@ -2450,13 +2450,8 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
         // B scenario slots per workgroup (PHGPU_STREAM_SLOTS=1|2, default 2)
         const char* env = getenv("PHGPU_STREAM_SLOTS");
         const int B = (env && atoi(env) == 1) ? 1 : 2;
-        // PHGPU_STREAM_PAIR=1: each wave takes two slices of its list per step (sell_dot_b2)
-        const char* pe = getenv("PHGPU_STREAM_PAIR");
-        const bool pair = pe ? atoi(pe) == 1 : false;
-        const void* fn = B == 1 ? (pair ? (const void*)k_solve_stream<1, false, true> : (const void*)k_solve_stream<1>)
-                                : (pair ? (const void*)k_solve_stream<2, false, true> : (const void*)k_solve_stream<2>);
-        int occ_pair = 0;
-        int& oc = pair ? occ_pair : h->occ_cache[B == 1 ? 4 : 5];
+        const void* fn = B == 1 ? (const void*)k_solve_stream<1> : (const void*)k_solve_stream<2>;
+        int& oc = h->occ_cache[B == 1 ? 4 : 5];
         if (!oc) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, SBLK, 0));
         per_cu = oc;
         // PHGPU_STREAM_PER_CU=k: launch k workgroups per CU whatever the occupancy query says
@@ -2511,15 +2506,9 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
                                               0, st));
         }
         nblk = std::min<int64_t>(nblk, std::max<int64_t>((h->S - T + B - 1) / B, 1));
-        if (B == 1 && pair)
-            hipLaunchKernelGGL((k_solve_stream<1, false, true>), dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead,
-                               x, y, obj, bound, status, iters, T, (double*)nullptr, 0u);
-        else if (B == 1)
+        if (B == 1)
             hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters, T, (double*)nullptr, 0u);
-        else if (pair)
-            hipLaunchKernelGGL((k_solve_stream<2, false, true>), dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead,
-                               x, y, obj, bound, status, iters, T, (double*)nullptr, 0u);
         else
             hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
                                bound, status, iters, T, (double*)nullptr, 0u);

@@ -229,37 +229,3 @@ def test_path4_split_matches_queue_on_aircond(gpu):
         assert np.allclose(res[0][1], ob, rtol=1e-6, atol=1e-6), (res[0][1], ob)
     # the wrapped-counter run takes the same branches: bit-identical to the plain split run
     assert np.array_equal(res[1][1], res[2][1])
-
-
-@pytest.mark.parametrize("slots", ["1", "2"])
-def test_path4_pair_form_is_bitwise_the_same(gpu, slots):
-    """PHGPU_STREAM_PAIR=1 (each wave takes two slices of its list per step, sell_dot_b2)
-    sums every row / column in the same order as the one-slice loop: cold and warm solves
-    of the UC scenarios give the same bits, for one and two slots per workgroup."""
-    from mpisppy_amd import _lib
-    from mpisppy_amd.engine import PHEngine
-    from mpisppy_amd.examples import uc
-    names = GOLD["names"]
-    b = uc.batch_creator(names, num_scens=GOLD["num_scens"])
-    keep = {k: os.environ.get(k) for k in ("PHGPU_STREAM_PAIR", "PHGPU_STREAM_SLOTS")}
-    out = {}
-    try:
-        os.environ["PHGPU_STREAM_SLOTS"] = slots
-        for pair in ("0", "1"):
-            os.environ["PHGPU_STREAM_PAIR"] = pair
-            e = PHEngine(b, device="cuda:0")
-            assert e.kernel_info()["path"] == 4
-            e.solve(_lib.default_options(eps_rel=UC_EPS, max_iter=4096), warm=False)
-            r = [e.host(k).copy() for k in ("x", "obj", "iters", "status")]
-            e.solve(_lib.default_options(eps_rel=UC_EPS, max_iter=4096), warm=True)
-            r += [e.host(k).copy() for k in ("x", "obj", "iters")]
-            out[pair] = r
-            e.close()
-    finally:
-        for k, v in keep.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    for a, c in zip(out["0"], out["1"]):
-        np.testing.assert_array_equal(a, c)
