@@ -59,7 +59,8 @@ def run(size, steps, comm):
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
             "batch_creator": farmer.batch_creator, "iterk_solver_options": {"beta_sufficient": 0.6},
             "iter0_solver_options": {"eps_rel": 1e-9}}
-    kw = {"crops_multiplier": 1, "num_scens": S}
+    # (the one-rank run on the share: probabilities 1/share, the same scenario data)
+    kw = {"crops_multiplier": 1, "num_scens": S if comm is not None else S // size}
     ph = PH(opts, names, farmer.scenario_creator, scenario_creator_kwargs=kw, mpicomm=comm)
     ph.PH_Prep()
     ph.Iter0()
