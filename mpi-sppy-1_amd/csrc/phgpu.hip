@@ -1002,9 +1002,12 @@ __device__ __forceinline__ void xp_recompute(const phgpu_state& st, const double
 }
 
 #define XF_THREADS 256
+// assign: node_buf was not cleared (one tree node, every entry is some nonant's): the fast
+// path stores its sums instead of adding them (phgpu_ph_reduce: one launch less per step)
 __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, double* __restrict__ node_buf,
                                                            const int32_t* __restrict__ dirty = nullptr,
-                                                           int xpC = 0, const double* __restrict__ x = nullptr) {
+                                                           int xpC = 0, const double* __restrict__ x = nullptr,
+                                                           int assign = 0) {
     __shared__ int fnode[XF_THREADS], lnode[XF_THREADS];
     __shared__ double fa[XF_THREADS], fb[XF_THREADS], la[XF_THREADS], lb[XF_THREADS];
     const int k = blockIdx.x;
@@ -1083,7 +1086,10 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
         if (t == 0) {
             int g0 = -1;
             for (int u = 0; u < XF_THREADS && g0 < 0; ++u) g0 = fnode[u] >= 0 ? fnode[u] : lnode[u];
-            if (g0 >= 0) {
+            if (g0 >= 0 && assign) {
+                node_buf[g0 * st.nlen_max + off] = fa[0];
+                node_buf[half + g0 * st.nlen_max + off] = fb[0];
+            } else if (g0 >= 0) {
                 node_buf[g0 * st.nlen_max + off] += fa[0];
                 node_buf[half + g0 * st.nlen_max + off] += fb[0];
             }
@@ -2891,10 +2897,12 @@ extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf
     if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
                                ? 0 : set_err(-2, "hipMemsetAsync failed");
     if (xp_valid(h, x)) {
-        // the solve's epilogue wrote the per-chunk partials: clear node_buf, final sums
-        HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
+        // the solve's epilogue wrote the per-chunk partials: final sums.  With one tree node
+        // every node_buf entry is a nonant's (its block stores it); else clear it first
+        const int assign = (h->num_nodes == 1 && h->nlen_max == h->nn) ? 1 : 0;
+        if (!assign) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
         hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, xp_view(h), node_buf,
-                           (const int32_t*)h->xp_dirty[h->wslot], h->xp_C[h->wslot], x);
+                           (const int32_t*)h->xp_dirty[h->wslot], h->xp_C[h->wslot], x, assign);
         HIPCHK(hipGetLastError());
         return 0;
     }

@@ -82,6 +82,9 @@ def run(size, steps, comm):
 def main():
     size = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    if len(sys.argv) > 3 and sys.argv[3] == "loopback":  # (under a profiler: that run alone)
+        print(f"loopback {size} ranks:", run(size, steps, LoopbackComm(size)), flush=True)
+        return
     print("one rank (folded step):", run(size, steps, None), flush=True)
     print(f"loopback {size} ranks (reduce / all-reduce / update, side-stream conv):",
           run(size, steps, LoopbackComm(size)), flush=True)
