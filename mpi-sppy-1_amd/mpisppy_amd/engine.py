@@ -545,18 +545,39 @@ class PHEngine:
         self.convergence_diff_async()
         return self.convergence_wait()
 
+    def convergence_mark(self):
+        """Mark the update on the launch stream (several ranks): a following
+        ``convergence_diff_async`` waits for this point rather than for whatever was queued
+        in between, so PHBase.iterk_loop launches the speculative solve right after the mark
+        and issues the side-stream conv work behind it -- the host's side-stream calls (event,
+        stream switch, all-reduce, copy) no longer delay the solve's launch (a 35 us idle gap
+        per PH iteration in the loopback trace)."""
+        if self._conv_zero_copy or self.comm.size == 1:
+            return
+        if not self.overlap_conv:
+            # (the comparison case: the conv all-reduce stays ahead of the solve)
+            self.convergence_diff_async()
+            self._conv_issued = self._upd_seq
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._mark = (self._upd_seq, ev)
+
     def convergence_diff_async(self):
         """Start the same readback without waiting; ``convergence_wait`` returns it and work
         queued after this call does not delay it.  One rank: the update kernel stores conv
         into pinned memory itself.  Several ranks: the conv all-reduce (phbase.py:341) and
-        its copy into pinned memory run on a side stream behind the update, so the next
-        solve launches at once and only the x̄ all-reduce stays ahead of it."""
+        its copy into pinned memory run on a side stream behind the update (or behind
+        ``convergence_mark``), so the next solve launches at once and only the x̄ all-reduce
+        stays ahead of it."""
         self._conv_seq = self._upd_seq
-        if self._conv_zero_copy:
+        if self._conv_zero_copy or getattr(self, "_conv_issued", 0) == self._upd_seq:
             return
         main = torch.cuda.current_stream(self.device)
         if self._conv_ev is None:
             self._conv_ev = torch.cuda.Event()
+        mark = getattr(self, "_mark", None)
+        self._mark = None
         if not self.overlap_conv:
             # (the comparison case of the bench: the conv all-reduce ahead of the next solve on
             # the launch stream, as the reference's Allreduce sits in the loop)
@@ -566,8 +587,11 @@ class PHEngine:
             self._conv_ev.record(main)
             self._upd_marks[self._upd_seq] = self._conv_ev
             return
-        ev = torch.cuda.Event()
-        ev.record(main)
+        if mark is not None and mark[0] == self._upd_seq:
+            ev = mark[1]                           # recorded right after the update
+        else:
+            ev = torch.cuda.Event()
+            ev.record(main)
         self._upd_marks[self._upd_seq] = ev        # (also the update's marker for its stats)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)

@@ -301,9 +301,12 @@ class PHBase(SPOpt):
             finally:
                 self._defer_update = False
             if spec:
-                self.engine.convergence_diff_async()
+                # (several ranks: the update is marked, the solve launched, then the conv
+                # all-reduce issued on the side stream behind the mark)
+                self.engine.convergence_mark()
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
                                 gripe=False, verbose=verbose, speculative=True)
+                self.engine.convergence_diff_async()
                 self.conv = self.engine.convergence_wait()
             else:
                 self.conv = self.convergence_diff()
