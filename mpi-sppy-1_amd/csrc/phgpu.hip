@@ -2877,17 +2877,18 @@ static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipS
 
 // the path-6 epilogue partials of x when the last solve writing the current slot produced
 // them for this x buffer, else null
-static bool xp_valid(const phgpu_state* h, const double* x) {
-    const int k = h->wslot;
-    return h->xp[k] && h->xp_C[k] > 0 && h->xp_x[k] == x && h->xbar_mixed == 0;
+static bool xp_valid(const phgpu_state* h, const double* x, int k) {
+    return k >= 0 && h->xp[k] && h->xp_C[k] > 0 && h->xp_x[k] == x && h->xbar_mixed == 0;
 }
-static phgpu_state xp_view(const phgpu_state* h) {  // the state with part = the epilogue partials
+static bool xp_valid(const phgpu_state* h, const double* x) { return xp_valid(h, x, h->wslot); }
+static phgpu_state xp_view(const phgpu_state* h, int k) {  // the state with part = the epilogue partials
     phgpu_state v = *h;
-    v.part = h->xp[h->wslot];
-    v.part_node = h->xp_node[h->wslot];
-    v.nwaves = h->xp_n[h->wslot];
+    v.part = h->xp[k];
+    v.part_node = h->xp_node[k];
+    v.nwaves = h->xp_n[k];
     return v;
 }
+static phgpu_state xp_view(const phgpu_state* h) { return xp_view(h, h->wslot); }
 
 extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf, void* stream) {
     if (!h || !x || !node_buf) return set_err(-1, "null argument");
@@ -2896,13 +2897,16 @@ extern "C" int phgpu_ph_reduce(phgpu_handle h, const double* x, double* node_buf
     const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
     if (h->nn == 0) return hipMemsetAsync(node_buf, 0, nb * sizeof(double), st) == hipSuccess
                                ? 0 : set_err(-2, "hipMemsetAsync failed");
-    if (xp_valid(h, x)) {
+    // the current slot's solve, or a deferred solve not yet committed (x its output: the PH
+    // loop reduces a speculative solve's x ahead of its convergence test, engine.xbar_ahead)
+    const int k = xp_valid(h, x) ? h->wslot : (xp_valid(h, x, h->pending) ? h->pending : -1);
+    if (k >= 0) {
         // the solve's epilogue wrote the per-chunk partials: final sums.  With one tree node
         // every node_buf entry is a nonant's (its block stores it); else clear it first
         const int assign = (h->num_nodes == 1 && h->nlen_max == h->nn) ? 1 : 0;
         if (!assign) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
-        hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, xp_view(h), node_buf,
-                           (const int32_t*)h->xp_dirty[h->wslot], h->xp_C[h->wslot], x, assign);
+        hipLaunchKernelGGL(k_xbar_final, dim3(h->nn), dim3(XF_THREADS), 0, st, xp_view(h, k), node_buf,
+                           (const int32_t*)h->xp_dirty[k], h->xp_C[k], x, assign);
         HIPCHK(hipGetLastError());
         return 0;
     }

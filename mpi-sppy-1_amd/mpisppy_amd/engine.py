@@ -179,6 +179,7 @@ class PHEngine:
         self._conv_seq = 0        # the update whose conv the pending readback returns
         self._conv_seen = 0       # the last update whose conv (and statistics) the host has seen
         self._side = None         # side stream of the conv all-reduce (several ranks)
+        self._ahead_id = 0        # launch whose x xbar_ahead reduced into node_buf (0: none)
         self._conv_ev = None      # the event behind its copy to pinned memory
         self._wait_stats = None   # the pinned statistics row the pending update writes (one rank)
         # markers: the event behind an update (by update number), recorded lazily, only when
@@ -473,16 +474,36 @@ class PHEngine:
         """Local partials + cross-rank sum (phbase.py:27-87); result left in node_buf.
         ``lazy`` (PHBase.Compute_Xbar with one rank): nothing is launched yet -- the next
         ``update`` does x̄ and the update together (phgpu_ph_step_local: one launch fewer
-        for two-stage problems); anything that reads node_buf first computes it."""
+        for two-stage problems); anything that reads node_buf first computes it.  Several
+        ranks: nothing to do when ``xbar_ahead`` already reduced the current solve's x."""
         if lazy and self.comm.size == 1:
             self._xbar_pending = True
             return None
         self._xbar_pending = False
+        if self._ahead_id and self._ahead_id == self._cur_id:
+            self._ahead_id = 0
+            return self.node_buf
+        self._ahead_id = 0
         self.compute_xbar_partials()
         if self.comm.size > 1:
             self.calls["allreduce_xbar"] += 1
         self._allreduce_sum_(self.node_buf)
         return self.node_buf
+
+    def xbar_ahead(self):
+        """Several ranks (PHBase.iterk_loop): reduce the speculative solve's x and start the x̄
+        all-reduce before the convergence test of the current iteration is known, so the next
+        iteration's x̄ is on its way when the host returns from the test.  Used by the next
+        ``compute_xbar`` if that solve is committed; dropped otherwise (node_buf is scratch,
+        and every rank issues the same collectives in the same order)."""
+        if self.comm.size == 1 or not hasattr(self, "_spec"):
+            return
+        self.calls["ph_reduce"] += 1
+        _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self._spec["x"]), _ptr(self.node_buf), self._stream()),
+                   "phgpu_ph_reduce")
+        self.calls["allreduce_xbar"] += 1
+        self._allreduce_sum_(self.node_buf)
+        self._ahead_id = self._spec_id
 
     def _flush_xbar(self):
         self._flush_step()

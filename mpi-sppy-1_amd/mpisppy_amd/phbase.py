@@ -307,6 +307,8 @@ class PHBase(SPOpt):
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=dtiming,
                                 gripe=False, verbose=verbose, speculative=True)
                 self.engine.convergence_diff_async()
+                if self.options.get("xbar_ahead", True):
+                    self.engine.xbar_ahead()
                 self.conv = self.engine.convergence_wait()
             else:
                 self.conv = self.convergence_diff()

@@ -2,7 +2,7 @@
 # Round 5, pass o (and p: the next x̄ reduced ahead of the convergence test): the speculative solve launched before the side-stream conv work (several
 # ranks): the multi-rank tests, loopback timings and trace, the 2-rank gloo bench line.
 cd "$(dirname "$0")/../.." || exit 1
-O=gpurun_out/r5o
+O=gpurun_out/r5p
 mkdir -p $O
 export TMPDIR=/tmp
 step() { n=$1; t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; r=$?; echo "$n rc=$r"; tail -3 $O/$n.log; [ $r -eq 0 ] || exit $r; }
