@@ -122,7 +122,7 @@ class PHEngine:
         _track(self)
         # library calls of the PH step, by kind (tests assert which path a loop took)
         self.calls = {"ph_reduce": 0, "ph_update_ex": 0, "ph_step_local": 0, "ph_step_defer": 0,
-                      "allreduce_xbar": 0, "allreduce_conv_side": 0, "allreduce_conv_main": 0}
+                      "allreduce_xbar": 0, "allreduce_conv_side": 0, "allreduce_conv_main": 0, "xbar_ahead_used": 0}
         # several ranks: the conv all-reduce on a side stream under the next solve (False: on
         # the launch stream ahead of it -- bench.py --no-conv-overlap, the comparison case)
         self.overlap_conv = True
@@ -482,6 +482,8 @@ class PHEngine:
         self._xbar_pending = False
         if self._ahead_id and self._ahead_id == self._cur_id:
             self._ahead_id = 0
+            self.node_buf, self._node_ahead = self._node_ahead, self.node_buf
+            self.calls["xbar_ahead_used"] += 1
             return self.node_buf
         self._ahead_id = 0
         self.compute_xbar_partials()
@@ -494,15 +496,18 @@ class PHEngine:
         """Several ranks (PHBase.iterk_loop): reduce the speculative solve's x and start the x̄
         all-reduce before the convergence test of the current iteration is known, so the next
         iteration's x̄ is on its way when the host returns from the test.  Used by the next
-        ``compute_xbar`` if that solve is committed; dropped otherwise (node_buf is scratch,
-        and every rank issues the same collectives in the same order)."""
+        ``compute_xbar`` if that solve is committed (its buffer then becomes node_buf), dropped
+        otherwise; node_buf keeps the x̄ of the last update meanwhile (xbar_by_node after the
+        loop), and every rank issues the same collectives in the same order."""
         if self.comm.size == 1 or not hasattr(self, "_spec"):
             return
+        if getattr(self, "_node_ahead", None) is None:
+            self._node_ahead = torch.zeros_like(self.node_buf)
         self.calls["ph_reduce"] += 1
-        _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self._spec["x"]), _ptr(self.node_buf), self._stream()),
+        _lib.check(self.lib.phgpu_ph_reduce(self.h, _ptr(self._spec["x"]), _ptr(self._node_ahead), self._stream()),
                    "phgpu_ph_reduce")
         self.calls["allreduce_xbar"] += 1
-        self._allreduce_sum_(self.node_buf)
+        self._allreduce_sum_(self._node_ahead)
         self._ahead_id = self._spec_id
 
     def _flush_xbar(self):

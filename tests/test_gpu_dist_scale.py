@@ -173,13 +173,17 @@ def _spawn(case, tmp_path):
 
 def _assert_multirank_step(rec, iters, lanes):
     """Path 6 on its expected lane count, every PH step through reduce -> all-reduce ->
-    update_ex with the conv all-reduce on the side stream, nothing folded or fused."""
+    update_ex with the conv all-reduce on the side stream, nothing folded or fused, the next
+    x̄ reduced ahead of each convergence test."""
     assert rec["path"] == 6 and rec["compiled"] == 1 and rec["scratch"] <= 1024, rec
     assert rec["lanes"] == lanes, rec
     c = rec["calls"]
     assert c["ph_reduce"] >= iters and c["allreduce_xbar"] == c["ph_reduce"], c
     assert c["ph_update_ex"] == iters and c["allreduce_conv_side"] == iters, c
     assert c["ph_step_local"] == 0 and c["ph_step_defer"] == 0 and rec["folded"] == 0, (c, rec)
+    # from the second PH iteration on, x̄ was reduced ahead of the convergence test
+    # (engine.xbar_ahead on the speculative solve's x, used once that solve is committed)
+    assert c["xbar_ahead_used"] >= iters - 1, c
 
 
 def _global_rows(r, sample):
