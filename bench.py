@@ -485,6 +485,9 @@ def main():
     if a.model == "farmer" and not a.default_solver_options:
         # the example's recommended PH-solve options (examples/farmer.py PDHG_ITERK_OPTIONS)
         opts["iterk_solver_options"].update(farmer.PDHG_ITERK_OPTIONS)
+    if a.model == "uc" and not a.default_solver_options:
+        from mpisppy_amd.examples import uc as _uc
+        opts["iterk_solver_options"].update(_uc.PDHG_ITERK_OPTIONS)
     for kv in a.solver_opt:
         k, v = kv.split("=", 1)
         opts["iterk_solver_options"][k] = float(v) if any(ch in v for ch in ".e") else int(v)

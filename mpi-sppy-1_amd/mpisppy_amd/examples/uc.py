@@ -34,6 +34,13 @@ BIG_PENALTY = 1e6              # ReferenceModel_OK.py:995-999
 MODERATELY_BIG_PENALTY = 1e5
 INITIAL_TIME = 1               # :133
 
+# Recommended options of the warm-started PH solves (path 4): restart once the fixed-point
+# residual fell to 0.7 of its value at the last restart (library default 0.2).  Config 5,
+# two timed PH iterations on one trajectory: mean PDHG iterations 15,836 (0.2) / 15,063
+# (0.4) / 13,718 (0.6) / 13,203 (0.7) / 13,973 (0.8), mean PH iteration 39.4 / 36.8 / 34.3
+# / 32.7 / 36.8 s (profiles/r05/s, t).
+PDHG_ITERK_OPTIONS = {"beta_sufficient": 0.7}
+
 
 # ---------------------------------------------------------------- data
 _ROOT_CACHE = {}

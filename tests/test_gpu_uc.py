@@ -54,17 +54,22 @@ def test_uc_lp_relaxation_vs_highs(gpu):
     e.close()
 
 
-def test_uc_ph_iterations(gpu):
+@pytest.mark.parametrize("tuned", [False, True])
+def test_uc_ph_iterations(gpu, tuned):
     """Three PH iterations of config 5 on 8 scenarios (uc_funcs.py rho setter): every
-    subproblem solved, W moves, the PH objective terms reach the kernel."""
+    subproblem solved, W moves, the PH objective terms reach the kernel -- with the library's
+    options and with the example's recommended PH-solve options (the bench's)."""
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import uc
     names = GOLD["names"]
     rho = uc.rho_vector(uc.scenario_creator(names[0], num_scens=GOLD["num_scens"]))
+    iterk = {"eps_rel": UC_EPS}
+    if tuned:
+        iterk.update(uc.PDHG_ITERK_OPTIONS)
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 3, "defaultPHrho": 1.0, "convthresh": -1.0,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
             "batch_creator": uc.batch_creator, "rho_array": rho,
-            "iter0_solver_options": {"eps_rel": UC_EPS}, "iterk_solver_options": {"eps_rel": UC_EPS}}
+            "iter0_solver_options": {"eps_rel": UC_EPS}, "iterk_solver_options": iterk}
     ph = PH(opts, names, uc.scenario_creator, scenario_creator_kwargs={"num_scens": len(names)})
     conv, eobj, tb = ph.ph_main()
     e = ph.engine
