@@ -38,8 +38,10 @@ INITIAL_TIME = 1               # :133
 # residual fell to 0.7 of its value at the last restart (library default 0.2).  Config 5,
 # two timed PH iterations on one trajectory: mean PDHG iterations 15,836 (0.2) / 15,063
 # (0.4) / 13,718 (0.6) / 13,203 (0.7) / 13,973 (0.8), mean PH iteration 39.4 / 36.8 / 34.3
-# / 32.7 / 36.8 s (profiles/r05/s, t).
-PDHG_ITERK_OPTIONS = {"beta_sufficient": 0.7}
+# / 32.7 / 36.8 s (profiles/r05/s, t); and the KKT test every 128 iterations instead of 64
+# (its two passes cost ~3% of the iterations; 13,439 mean iterations, 31.4 s; a restart test
+# every 32 or an artificial restart at 0.5 did not help, profiles/r05/v).
+PDHG_ITERK_OPTIONS = {"beta_sufficient": 0.7, "check_every": 128}
 
 
 # ---------------------------------------------------------------- data
