@@ -485,6 +485,9 @@ def main():
     if a.model == "farmer" and not a.default_solver_options:
         # the example's recommended PH-solve options (examples/farmer.py PDHG_ITERK_OPTIONS)
         opts["iterk_solver_options"].update(farmer.PDHG_ITERK_OPTIONS)
+    if a.model == "aircond" and not a.default_solver_options:
+        from mpisppy_amd.examples import aircond as _air
+        opts["ipm_tuning"] = dict(_air.IPM_TUNING)    # the model's interior-point constants
     if a.model == "uc" and not a.default_solver_options:
         from mpisppy_amd.examples import uc as _uc
         opts["iterk_solver_options"].update(_uc.PDHG_ITERK_OPTIONS)
@@ -609,6 +612,7 @@ def main():
                        "rho": a.rho, "eps_rel": a.eps,
                        "iterk_solver_options": {k: v for k, v in opts["iterk_solver_options"].items()
                                                 if k != "eps_rel"},
+                       "ipm_tuning": opts.get("ipm_tuning"),
                        "scenarios_per_gpu": b.S,
                        "n": b.n, "m": b.m, "nnz": b.nnz,
                        "conv_allreduce": (("launch stream, ahead of the next solve" if a.no_conv_overlap

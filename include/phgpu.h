@@ -163,6 +163,14 @@ int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
  * (no epilogue partials, no folded or fused step). */
 int phgpu_set_nonant_probs(phgpu_handle h, const double* pvar);
 
+/* Interior-point tuning of this handle (path 6): defs = "IPM_NAME=number;..." -- the
+ * compile-time constants of the generated interior-point modules (jit_ipm*.hip.in:
+ * IPM_SIG_MIN, IPM_WARM_T, ...) for the modules this handle builds; a model's measured
+ * values (examples/aircond.py IPM_TUNING).  Only IPM_ names and numeric values; NULL or ""
+ * clears.  Call before the first solve (-1 once the module is built).  The PHGPU_IPM_DEFS
+ * environment variable (experiments) overrides it name by name. */
+int phgpu_set_ipm_tuning(phgpu_handle h, const char* defs);
+
 /* Bind the PH objective terms for the next solves (phbase.py:585-699):
  *   objective = f(x) + W_on * sum_k W[k,s] x_k + prox_on * sum_k rho[k,s]/2 (x_k - xbar[k,s])^2
  * W, rho, xbar: device [nn*S]; they are read at solve time (not copied). */

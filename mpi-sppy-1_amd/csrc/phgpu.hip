@@ -24,6 +24,9 @@
 #include <algorithm>
 #include <chrono>
 #include <vector>
+#include <map>
+#include <string>
+#include <cctype>
 
 #include "phgpu.h"
 
@@ -3068,6 +3071,7 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
 
 extern "C" int phgpu_destroy(phgpu_handle h) {
     if (!h) return 0;
+    g_ipm_tuning_of.erase(h);
     h->pend.active = 0;  // a deferred step that never ran is dropped with the handle
     if (h->oms[0]) {  // the x / y / omega / sk_iters fields may be bound to slot 1: free by slot
         h->x = h->xs[0];

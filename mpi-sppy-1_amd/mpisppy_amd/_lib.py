@@ -50,7 +50,7 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats",
            "phgpu_ph_update_ex", "phgpu_ph_step_local", "phgpu_ph_step_defer", "phgpu_ph_step_flush",
-           "phgpu_set_nonant_probs"]
+           "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning"]
 
 _lib = None
 
@@ -75,6 +75,7 @@ def load(path=None):
     lib.phgpu_create2.argtypes = lib.phgpu_create.argtypes + [ctypes.c_uint32]
     lib.phgpu_set_scenarios.argtypes = [c_vp] + [c_vp] * 11 + [c_vp]
     lib.phgpu_set_nonant_probs.argtypes = [c_vp, c_vp]
+    lib.phgpu_set_ipm_tuning.argtypes = [c_vp, ctypes.c_char_p]
     lib.phgpu_set_ph_state.argtypes = [c_vp, c_vp, c_vp, c_vp, c_int, c_int]
     lib.phgpu_solve.argtypes = [c_vp, ctypes.POINTER(PhgpuOptions), c_int, c_vp, c_vp, c_vp, c_vp,
                                 c_vp, c_vp, c_vp]

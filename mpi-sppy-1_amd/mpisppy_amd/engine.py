@@ -256,6 +256,12 @@ class PHEngine:
         self._flush_step()
         self.W.copy_(_dev_T(np.asarray(W, dtype=np.float64), self.device))
 
+    def set_ipm_tuning(self, tuning):
+        """Interior-point constants for this handle's modules ({"IPM_SIG_MIN": 0.003, ...};
+        phgpu_set_ipm_tuning, before the first solve): a model's measured values."""
+        defs = ";".join(f"{k}={v if isinstance(v, int) else repr(float(v))}" for k, v in (tuning or {}).items())
+        _lib.check(self.lib.phgpu_set_ipm_tuning(self.h, defs.encode()), "phgpu_set_ipm_tuning")
+
     def set_nonant_probs(self, var_prob):
         """Per-nonant probability coefficients, host [S, nn] (SPBase.var_prob), or None:
         the x̄ weights and the Update_W mask of variable probabilities (phgpu_set_nonant_probs,

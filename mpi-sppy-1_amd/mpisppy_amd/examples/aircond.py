@@ -11,6 +11,13 @@ from ..sputils import extract_num, node_idx, create_nodenames_from_branching_fac
 from ..scenario_tree import ScenarioNode
 from ..batch import batch_from_models, ScenarioBatch
 
+# Interior-point constants measured for this model (PH option "ipm_tuning" ->
+# phgpu_set_ipm_tuning): a lower centring floor and a deeper warm-start push.  Config 4
+# (65,536 scenarios, one lane per scenario): 2,759-2,791 PH it/s against 2,556-2,576 with the
+# library's 0.01 / 0.1, max / mean IPM iterations per PH solve 18 / 7.7 against 20 / 7.9
+# (profiles/r05/x); farmer gains nothing from them (8,906-8,919 against 8,971-8,975).
+IPM_TUNING = {"IPM_SIG_MIN": 0.003, "IPM_WARM_T": 0.3}
+
 # aircond.py:19-35 ("Do not edit these defaults!")
 PARMS = {
     "mu_dev": 0.0, "sigma_dev": 40.0, "start_ups": False, "StartUpCost": 300.0,

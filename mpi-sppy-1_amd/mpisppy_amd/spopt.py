@@ -95,6 +95,9 @@ class SPOpt(SPBase):
                                    node_names=self.node_names, shared=self.options.get("shared_matrix"))
             if getattr(self, "var_prob", None) is not None:
                 self.engine.set_nonant_probs(self.var_prob)
+            if self.options.get("ipm_tuning"):
+                # a model's interior-point constants (e.g. examples/aircond.py IPM_TUNING)
+                self.engine.set_ipm_tuning(self.options["ipm_tuning"])
 
     # options the reference's cfg_vanilla.shared_options passes to MIP/LP plugins
     # (threads, mipgap; cfg_vanilla.py:41-62) or that only drive plugin output (Tee):

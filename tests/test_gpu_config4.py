@@ -160,12 +160,15 @@ def test_config4_aircond65536_vs_oracle(gpu, config4_path):
 
 @pytest.mark.skipif(not os.path.exists(CONV_FILE), reason="aircond_conv.json not generated")
 def test_config4_aircond65536_iterations_to_convergence(gpu):
-    """Config 4 on path 6 (the bench's kernel) by ph_main to conv < 1e-2: the oracle's PH
-    iteration count +-1 and x̄ of all 1,057 nodes at the break within 1e-5."""
+    """Config 4 on path 6 (the bench's kernel and interior-point constants) by ph_main to
+    conv < 1e-2: the oracle's PH iteration count +-1 and x̄ of all 1,057 nodes at the break
+    within 1e-5."""
     g = json.load(open(CONV_FILE))
     assert g["kwargs"] == KW and g["rho"] == 1.0
     want = g["break_iteration"]
-    ph = _aircond_ph(g["branching_factors"], want + 10, g["conv_thresh"])
+    from mpisppy_amd.examples import aircond
+    # (with the model's interior-point constants, as the bench runs config 4)
+    ph = _aircond_ph(g["branching_factors"], want + 10, g["conv_thresh"], ipm_tuning=aircond.IPM_TUNING)
     ph.ph_main()
     _assert_path6(ph)
     assert ph.converged and abs(ph._PHIter - want) <= 1, (ph._PHIter, want, g["conv"][-3:])
@@ -183,3 +186,30 @@ def test_config4_aircond65536_iterations_to_convergence(gpu):
         ref = np.array(g["W_break"])
         err = np.abs(W - ref) / np.maximum(1.0, np.abs(ref))
         assert err.max() <= ABS, (err.max(), np.abs(W - ref).max())
+
+
+def test_ipm_tuning_reaches_the_module_and_is_checked(gpu):
+    """phgpu_set_ipm_tuning: the definitions go into the handle's generated module (the
+    config-4 constants change the iteration counts), bad names / values and a call after
+    the module is built are refused."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import aircond
+    bf = [4, 8, 16]
+    b = aircond.batch_creator(aircond.scenario_names_creator(int(np.prod(bf))), branching_factors=bf, **KW)
+    its = []
+    for tun in (None, aircond.IPM_TUNING):
+        e = PHEngine(b, device="cuda:0")
+        if tun:
+            with pytest.raises(_lib.PhgpuError, match="not an IPM_ constant"):
+                e.set_ipm_tuning({"NC": 3})
+            with pytest.raises(_lib.PhgpuError, match="not a number"):
+                _lib.check(e.lib.phgpu_set_ipm_tuning(e.h, b"IPM_WARM_T=abc"), "phgpu_set_ipm_tuning")
+            e.set_ipm_tuning(tun)
+        e.solve(_lib.default_options(eps_rel=1e-9), warm=False)
+        assert e.kernel_info()["path"] == 6
+        its.append(e.host("iters").copy())
+        with pytest.raises(_lib.PhgpuError, match="already built"):
+            e.set_ipm_tuning(aircond.IPM_TUNING)
+        e.close()
+    assert not np.array_equal(its[0], its[1])
