@@ -40,7 +40,8 @@ INITIAL_TIME = 1               # :133
 # (0.4) / 13,718 (0.6) / 13,203 (0.7) / 13,973 (0.8), mean PH iteration 39.4 / 36.8 / 34.3
 # / 32.7 / 36.8 s (profiles/r05/s, t); and the KKT test every 128 iterations instead of 64
 # (its two passes cost ~3% of the iterations; 13,439 mean iterations, 31.4 s; a restart test
-# every 32 or an artificial restart at 0.5 did not help, profiles/r05/v).
+# every 32, an artificial restart at 0.5, a KKT test every 256 or a step fraction of 0.999
+# did not help, profiles/r05/v, cc).
 PDHG_ITERK_OPTIONS = {"beta_sufficient": 0.7, "check_every": 128}
 
 
