@@ -66,6 +66,11 @@ def parse():
                    help="extra phgpu_options for the PH solves (tuning), e.g. check_every=32")
     p.add_argument("--default-solver-options", action="store_true",
                    help="farmer: ignore the example's recommended PH-solve options (library defaults)")
+    p.add_argument("--check", choices=["auto", "on", "off"], default="auto",
+                   help="compare the warmup with the oracle fixture of the workload (farmer 65,536 cm=1, "
+                        "farmer 1,024 cm=10, aircond 32x32x64) and exit non-zero on a mismatch; auto: when "
+                        "the workload and rho match a fixture, on: whenever the workload has one (a "
+                        "different --rho then fails by design)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     p.add_argument("--profile-dir", default=None,
@@ -430,6 +435,106 @@ def _uc_cpu_worker(args):
     return time.perf_counter() - t
 
 
+# ---------------------------------------------------------------- self-check
+# The warmup iterations of a fixture workload are exactly the PH iterations the committed
+# oracle fixtures pin (tests/golden/make_golden_scale.py, make_golden_aircond.py): the
+# bench compares them on every rank before timing, so an N > 1 run (RCCL all-reduces of
+# the node buffer and of conv, phbase.py:83-87, 339-343) that computes a wrong x̄, W or
+# conv says so in its JSON line and exits non-zero.  Tolerances are north_star's.
+CHECK_REL = 1e-5
+CHECK_ABS = 1e-5
+CHECK_FIXTURES = {("farmer", 65536, 1): ("farmer_scale.json", "farmer65536_cm1"),
+                  ("farmer", 1024, 10): ("farmer_scale.json", "farmer1024_cm10"),
+                  ("aircond", 65536, None): ("aircond_scale.json", None)}
+
+
+def load_check_fixture(model, scens, cm, bf=None):
+    """The oracle fixture of this workload, or None (the bench then runs unchecked)."""
+    key = (model, scens, cm if model == "farmer" else None)
+    if key not in CHECK_FIXTURES:
+        return None
+    fname, sub = CHECK_FIXTURES[key]
+    path = os.path.join(ROOT, "tests", "golden", fname)
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    g = g[sub] if sub else g
+    if model == "aircond" and (bf is None or list(g["branching_factors"]) != list(bf)):
+        return None
+    return g
+
+
+def parity_checks(g, obs, rho):
+    """Compare one rank's view of the warmup with the oracle fixture ``g``.
+
+    ``obs``: trivial_bound; conv (the conv of each warmup PH iteration); xbar_last (the x̄
+    of the last warmup iteration, farmer: the ROOT vector, aircond: {node: vector});
+    w_rows ({global scenario index: W row} for this rank's scenarios); eobj (E[obj] after
+    the warmup); warmup.  Returns a dict of booleans and the largest errors.  A check the
+    warmup length does not reach (fewer iterations than the fixture pins) is None."""
+    k = int(obs["warmup"])
+    pinned = int(g["ph_iters"])
+    out = {"fixture_rho_ok": abs(float(rho) - float(g["rho"])) == 0.0}
+    tb, tb_ref = float(obs["trivial_bound"]), float(g["trivial_bound"])
+    out["trivial_bound_err_rel"] = abs(tb - tb_ref) / abs(tb_ref)
+    out["trivial_bound_ok"] = bool(out["trivial_bound_err_rel"] <= CHECK_REL)
+    n = min(k, pinned)
+    conv = np.asarray(obs["conv"][:n], dtype=float)
+    if n and len(conv) == n:
+        err = float(np.abs(conv - np.asarray(g["conv"][:n])).max())
+        out["conv_err"], out["conv_ok"] = err, bool(err <= CHECK_ABS)
+    else:
+        out["conv_err"], out["conv_ok"] = None, (None if n == 0 else False)
+    if k == pinned:
+        if isinstance(obs["xbar_last"], dict):            # multistage: every node of the fixture
+            got = np.array([np.asarray(obs["xbar_last"][nd])[:2] for nd in g["node_names"]])
+            ref = np.asarray(g["xbar"][pinned - 1])
+        else:
+            ref = np.asarray(g["xbar"][pinned - 1])
+            got = np.asarray(obs["xbar_last"])[:len(ref)]
+        err = float(np.abs(got - ref).max())
+        out["xbar_err"], out["xbar_ok"] = err, bool(err <= CHECK_ABS)
+        smp = list(g["sample"])
+        pos = {s: j for j, s in enumerate(smp)}
+        mine = [s for s in obs["w_rows"] if s in pos]
+        if mine:
+            got = np.array([np.asarray(obs["w_rows"][s]) for s in mine])
+            ref = np.array([g["W"][pos[s]] for s in mine])[:, :got.shape[1]]
+            err = float(np.abs(got[:, :ref.shape[1]] - ref).max())
+            out["W_err"], out["W_ok"], out["W_rows"] = err, bool(err <= CHECK_ABS), len(mine)
+        else:
+            out["W_err"], out["W_ok"], out["W_rows"] = 0.0, True, 0
+        err = abs(float(obs["eobj"]) - float(g["Eobj"])) / abs(float(g["Eobj"]))
+        out["eobj_err_rel"], out["eobj_ok"] = err, bool(err <= CHECK_REL)
+    else:
+        for key in ("xbar", "W", "eobj"):
+            out[key + "_ok"] = None
+    return out
+
+
+def combine_checks(per_rank, world_size, backend):
+    """Fold the ranks' parity_checks dicts into the JSON line's ``checks``: every boolean
+    must hold on every rank (None = not reached by this warmup), errors are maxima, and
+    the ranks must agree on conv bit for bit (they read the same all-reduced value)."""
+    keys = [k for k in per_rank[0] if k.endswith("_ok")]
+    out = {"world_size": world_size, "backend": backend, "ranks_seen": len(per_rank)}
+    for key in keys:
+        vals = [r[key] for r in per_rank]
+        out[key] = None if all(v is None for v in vals) else all(bool(v) for v in vals if v is not None) \
+            and not any(v is None for v in vals)
+    for key in per_rank[0]:
+        if key.endswith("_err") or key.endswith("_err_rel"):
+            vals = [r[key] for r in per_rank if r[key] is not None]
+            out[key] = max(vals) if vals else None
+    out["W_rows_checked"] = sum(int(r.get("W_rows", 0) or 0) for r in per_rank)
+    convs = [tuple(r.get("conv_seen", ())) for r in per_rank]
+    out["ranks_agree_on_conv"] = all(c == convs[0] for c in convs)
+    out["ranks_seen_ok"] = out["ranks_seen"] == world_size
+    verdict = [v for k, v in out.items() if k.endswith("_ok") and k != "fixture_rho_ok"]
+    out["all_ok"] = bool(all(v is not False for v in verdict) and out["ranks_agree_on_conv"])
+    return out
+
+
 # ---------------------------------------------------------------- GPU run
 def main():
     a = parse()
@@ -547,8 +652,38 @@ def main():
         # the PMC summaries under profiles/ are per GPU instance: keyed by the scenarios
         # one rank holds (its kernel instance / lane count depend on it)
         tag = {"farmer": f"farmer{b.S}_cm{a.cm}", "uc": f"uc{b.S}", "aircond": f"aircond{b.S}"}[a.model]
+        fixture = None
+        if a.check != "off" and a.warmup > 0:
+            fixture = load_check_fixture(a.model, a.scens, a.cm, a.bf if a.model == "aircond" else None)
+            if fixture is not None and a.check == "auto" and float(fixture["rho"]) != a.rho:
+                fixture = None
+        conv_seen = []
+        if fixture is not None:
+            # keep each warmup iteration's conv (the engine's readback, both loop variants)
+            _wait, _diff = e.convergence_wait, e.convergence_diff
+            e.convergence_wait = lambda: conv_seen.append(_wait()) or conv_seen[-1]
+            e.convergence_diff = lambda: conv_seen.append(_diff()) or conv_seen[-1]
         ph.iterk_loop()                                # W warmup iterations (untimed)
         torch.cuda.synchronize()
+        checks = None
+        if fixture is not None:
+            del e.convergence_wait, e.convergence_diff     # back to the class methods
+            nx = ph.xbar_by_node()
+            first = names.index(ph.local_scenario_names[0])      # contiguous slices (sputils.py:803-810)
+            Wl = ph.W_array()
+            obs = {"trivial_bound": trivial_bound, "conv": conv_seen, "warmup": a.warmup,
+                   "xbar_last": (nx["ROOT"] if a.model == "farmer" else nx),
+                   "w_rows": {first + i: Wl[i] for i in range(Wl.shape[0])},
+                   "eobj": ph.Eobjective()}
+            mine = parity_checks(fixture, obs, a.rho)
+            mine["conv_seen"] = [float(v) for v in conv_seen]
+            checks = combine_checks(comm.allgather_object(mine),
+                                    dist.get_world_size() if world > 1 else 1,
+                                    backend if world > 1 else "none (one rank)")
+            checks["fixture"] = " / ".join(x for x in CHECK_FIXTURES[(a.model, a.scens, a.cm if a.model == "farmer"
+                                                                     else None)] if x)
+            checks["tolerance"] = {"rel": CHECK_REL, "abs": CHECK_ABS}
+            log("[bench] checks:", json.dumps(checks))
         log(f"[bench] warmup done ({time.perf_counter() - t_setup:.1f} s)")
         t_setup = time.perf_counter() - t_setup
         # HIP events around one solve launch in INSTRUMENT_EVERY (each event is a marker
@@ -584,7 +719,11 @@ def main():
     ws = e.workspace_bytes() + 8 * (b.S * (b.n + b.m + 3 * max(b.nn, 1) + 4))
     ipm_diag = e.ipm_info()
     rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir, ipm=ipm_diag)
-    ph_its = 1.0 / med               # median of iterations 2..K
+    # value: K timed PH iterations / the synchronised wall time of the whole timed region
+    # (barrier + synchronize on both sides, max over ranks) -- every GPU iteration counted,
+    # including the speculative solve's overlap; the median of the host's per-iteration
+    # times (BASELINE.md section 2's definition) is kept beside it
+    ph_its = a.steps / elapsed
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -593,11 +732,12 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": 1e3 * med,
-            "ms_per_step_definition": "median of the per-iteration wall times of timed PH iterations 2..K "
-                                      "(BASELINE.md section 2), max over ranks",
-            "ms_per_step_mean": 1e3 * elapsed / a.steps,
-            "value_from_mean": a.steps / elapsed,
+            "ms_per_step": 1e3 * elapsed / a.steps,
+            "ms_per_step_definition": "synchronised wall time of the K timed PH iterations / K (barrier + "
+                                      "device synchronize on both sides), max over ranks",
+            "ms_per_step_median": 1e3 * med,
+            "value_from_median": 1.0 / med,
+            "checks": checks,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -628,7 +768,7 @@ def main():
                               "allreduce": float(ar_ms[0].item()),
                               # the conv all-reduce, on a side stream under the next solve
                               "allreduce_overlapped": float(ar_ms[1].item()),
-                              "rest_of_step": 1e3 * med - rl["launch_ms"] - float(ar_ms[0].item())},
+                              "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"] - float(ar_ms[0].item())},
             "instrumented_solves": {"count": n_ins, "every": INSTRUMENT_EVERY,
                                     "note": "HIP events around every INSTRUMENT_EVERY-th timed solve launch "
                                             "(roofline launch_ms); the other timed steps carry no markers"},
@@ -663,6 +803,9 @@ def main():
     e.close()
     if world > 1:
         dist.destroy_process_group()
+    if checks is not None and not checks["all_ok"]:
+        log("[bench] PARITY CHECK FAILED:", json.dumps(checks))
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -160,7 +160,7 @@ int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const double* c,
  * sums in place of the per-node prob_coeff; Update_W then sets W[k,s] = 0 where pvar[k,s]
  * is 0 (prob0_mask).  Read at every reduce / update (not copied); NULL restores the per-node
  * coefficients.  While set, the PH step always runs as phgpu_ph_reduce + phgpu_ph_update
- * (no epilogue partials, no folded or fused step). */
+ * (no epilogue partials, no folded or fused step); partials of earlier solves are dropped. */
 int phgpu_set_nonant_probs(phgpu_handle h, const double* pvar);
 
 /* Interior-point tuning of this handle (path 6): defs = "IPM_NAME=number;..." -- the

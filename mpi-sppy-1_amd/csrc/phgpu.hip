@@ -2351,7 +2351,12 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
 extern "C" int phgpu_set_nonant_probs(phgpu_handle h, const double* pvar) {
     FLUSH_STEP(h);
     if (!h) return set_err(-1, "null handle");
-    h->pvar = h->nn > 0 ? pvar : nullptr;
+    const double* nv = h->nn > 0 ? pvar : nullptr;
+    // the path-6 epilogue partials of both slots were weighted with the per-node prob_coeff
+    // (or the previous pvar, whose values the caller may have rewritten in place): a later
+    // phgpu_ph_reduce must not take them for this x
+    h->xp_C[0] = h->xp_C[1] = 0;
+    h->pvar = nv;
     return 0;
 }
 
@@ -3186,7 +3191,10 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     // the subtree kernel's jam statistics of the last path-6 solve (synchronous read)
     if (h->last_stats && h->ipm_stats && h->last_path == 6) {
         unsigned long long st8[8];
-        if (hipMemcpy(st8, h->last_stats, sizeof(st8), hipMemcpyDeviceToHost) == hipSuccess) {
+        // the solve may still run on a non-blocking stream (a torch side stream, the
+        // speculative launch), which hipMemcpy does not wait for: finish it first
+        if (hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(st8, h->last_stats, sizeof(st8), hipMemcpyDeviceToHost) == hipSuccess) {
             info[13] = (double)st8[6];
             info[14] = (double)st8[7];
         }

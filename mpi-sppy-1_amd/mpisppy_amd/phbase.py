@@ -250,6 +250,13 @@ class PHBase(SPOpt):
         while n < self.ITER0_CONTINUATIONS:
             st = self.engine.host("status")
             lim = int((st == _lib.ITER_LIMIT).sum())
+            if self.n_proc > 1:
+                # every rank runs the same number of continuation solve_loops (an extension's
+                # pre / post_solve_loop may hold a collective)
+                import torch
+                t = torch.tensor([float(lim)], dtype=torch.float64, device=self.engine.device)
+                self.mpicomm.allreduce_max_(t)
+                lim = int(t.item())
             if lim == 0:
                 break
             opts = dict(self.current_solver_options)

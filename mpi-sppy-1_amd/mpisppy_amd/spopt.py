@@ -46,7 +46,15 @@ class ScenarioResults:
         self.solver = self._Solver(_TERMINATION.get(self.status, "error"))
         lo, up = (bound, obj) if sense > 0 else (obj, bound)
         self.Problem = [self._Problem(float(lo), float(up))]
-        self.solution = [self] if self.status in (_lib.OPTIMAL, _lib.ITER_LIMIT) else []
+        self.solution = _SolutionSet([self] if self.status in (_lib.OPTIMAL, _lib.ITER_LIMIT) else [])
+
+
+class _SolutionSet(list):
+    """``results.solution`` of a Pyomo results object: indexable and callable
+    (``results.solution(0)``); empty for an infeasible / unbounded solve."""
+
+    def __call__(self, i=0):
+        return self[i]
 
 
 class ScenarioView:
@@ -158,10 +166,11 @@ class SPOpt(SPBase):
         self.load_solutions_to_models()
         st, obj, bd, it = (self.engine.host(k) for k in ("status", "obj", "bound", "iters"))
         sense = self.batch.sense
+        # spopt.py:165-221: the results object with termination 'infeasible' / 'unbounded'
+        # (and no solution) for a certified failure; None only where the solver raised,
+        # which a batched launch does not do per scenario
         for k, sp in enumerate(self._subproblems()):
-            failed = st[k] in (_lib.PRIMAL_INFEASIBLE, _lib.DUAL_INFEASIBLE)
-            res = None if failed else ScenarioResults(st[k], sense * obj[k], sense * bd[k], it[k], sense)
-            ext.post_solve(sp, res)
+            ext.post_solve(sp, ScenarioResults(st[k], sense * obj[k], sense * bd[k], it[k], sense))
 
     def gripe_report(self):
         """The gripe of a solve_loop(gripe="deferred") (spopt.py:284-294 prints it right

@@ -1,7 +1,8 @@
 """Per-scenario extension hooks pre_solve / post_solve (spopt.py:146-147, 220-221;
 extensions/extension.py:18-45): they bracket the batched solve, once per local scenario per
 solve_loop, post_solve with the scenario's solution loaded and a results object in the
-Pyomo shape (termination condition, Lower_bound / Upper_bound), None for a failed solve.
+Pyomo shape (termination condition, Lower_bound / Upper_bound; 'infeasible' / 'unbounded'
+with an empty solution for a certified failure).
 
 CPU: which hooks an extension overrides (the loop keeps its speculative solve unless a hook
 that needs the reference's order is defined).  GPU: farmer (per-scenario models) and the
@@ -116,3 +117,18 @@ def test_hooks_on_a_batch_creator(gpu):
     assert [e[1] for e in post] == ph.local_scenario_names
     v = ScenarioView(ph, 5, ph.local_scenario_names[5])
     np.testing.assert_array_equal(v.x, ph.engine.host("x")[5])
+
+
+def test_results_object_for_failed_and_optimal_solves():
+    """a certified infeasible / unbounded scenario gets a results object with that
+    termination condition and an empty solution (spopt.py:165-221), not None; the solution
+    set is callable like Pyomo's (results.solution(0))."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.spopt import ScenarioResults
+    r = ScenarioResults(_lib.PRIMAL_INFEASIBLE, float("inf"), float("inf"), 600)
+    assert r.solver.termination_condition == "infeasible" and len(r.solution) == 0 and not r.solution
+    r = ScenarioResults(_lib.DUAL_INFEASIBLE, -float("inf"), -float("inf"), 600)
+    assert r.solver.termination_condition == "unbounded" and r.solver.status == "warning"
+    r = ScenarioResults(_lib.OPTIMAL, 3.0, 2.5, 7, sense=-1)
+    assert r.solution(0) is r and r.solution[0] is r
+    assert (r.Problem[0].Lower_bound, r.Problem[0].Upper_bound) == (3.0, 2.5)

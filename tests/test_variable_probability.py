@@ -168,3 +168,35 @@ def test_aircond_stage2_setter_and_sum_check():
     for k in range(b.nn):
         if k != k2[0]:
             np.testing.assert_allclose(ph.var_prob[:, k], b.prob_coeff[:, b.nonant_depth[k]])
+
+
+@pytest.mark.gpu
+def test_probabilities_set_after_a_path6_solve_drop_its_partials(gpu):
+    """the path-6 epilogue x̄ partials of a solve are weighted with the node's
+    prob_coeff; probabilities installed after that solve must not be reduced from them.
+    Iter0 on 256 farmer scenarios (path 6 writes the partials), then per-nonant weights,
+    then phgpu_ph_reduce: x̄ equals sum_s p_ks x_ks of the solved x."""
+    from mpisppy_amd.opt.ph import PH
+    from mpisppy_amd.examples import farmer
+    S = 256
+    opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 1, "defaultPHrho": 1.0, "convthresh": -1.0,
+            "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
+            "batch_creator": farmer.batch_creator}
+    ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+            scenario_creator_kwargs={"num_scens": S})
+    ph.PH_Prep()
+    ph.Iter0()
+    e = ph.engine
+    assert e.kernel_info()["path"] == 6
+    x = e.nonant_x()                                   # [S, nn]
+    rng = np.random.default_rng(3)
+    vp = rng.random((S, x.shape[1]))
+    vp[5, :] = 0.0
+    vp /= vp.sum(0, keepdims=True)
+    e.set_nonant_probs(vp)
+    e.compute_xbar()
+    xb = e.node_xbar()["ROOT"][:x.shape[1]]
+    want = (vp * x).sum(0)
+    assert np.abs(xb - want).max() <= 1e-9 * np.abs(want).max(), (xb, want)
+    plain = x.mean(0)
+    assert np.abs(xb - plain).max() > 1e-3            # the weights changed x̄ (not the stale partials)
