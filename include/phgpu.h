@@ -339,6 +339,14 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
  * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
+/* Diagnostics (no reference counterpart): the per-phase shader-clock cycle sums of the
+ * lane-group interior point's iteration loop, out[16] -- out[0..7] phases (slacks / mu,
+ * A x and A'y, KKT test, normal-equation assembly, factorisation, right-hand side + solve,
+ * dx / dw, step lengths + update), out[14] waves, out[15] loop trips -- accumulated by
+ * modules compiled with IPM_PROF=1 (PHGPU_IPM_DEFS) and zero otherwise; synchronises the
+ * device; reset != 0 clears them. */
+int phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int reset);
+
 /* The path-6 source the library generates for a pattern and its data flags (host code
  * only; tests and tools).  flags / v0 are per element of [A nnz | c n | q n | lb n | ub n |
  * rl m | ru m]: bit 0 the same value in every scenario, bit 1 finite in some scenario,

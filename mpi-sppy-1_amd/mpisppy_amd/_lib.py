@@ -50,7 +50,7 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats",
            "phgpu_ph_update_ex", "phgpu_ph_step_local", "phgpu_ph_step_defer", "phgpu_ph_step_flush",
-           "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning"]
+           "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning", "phgpu_ipm_prof"]
 
 _lib = None
 
@@ -96,6 +96,7 @@ def load(path=None):
     lib.phgpu_workspace_bytes.restype = c_i64
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
+    lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_int]
     lib.phgpu_solve_stats.argtypes = [c_vp, c_vp, c_vp]
     lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl), c_i32,
                                      ctypes.c_char_p, ctypes.c_size_t, P_i32]

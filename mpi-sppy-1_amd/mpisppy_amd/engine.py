@@ -238,6 +238,13 @@ class PHEngine:
                 "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel", "jam_handovers", "recentrings"]
         return dict(zip(keys, list(info)))
 
+    def ipm_prof(self, reset=True):
+        """Phase cycle sums of the lane-group interior point (diagnostics; modules built with
+        IPM_PROF=1 in PHGPU_IPM_DEFS, else zeros): phgpu_ipm_prof."""
+        out = (ctypes.c_ulonglong * 16)()
+        _lib.check(self.lib.phgpu_ipm_prof(self.h, out, 1 if reset else 0), "phgpu_ipm_prof")
+        return list(out)
+
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):
         """rho: scalar, host [nn] array (the same per-nonant rho in every scenario) or host

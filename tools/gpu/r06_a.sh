@@ -17,4 +17,11 @@ grep '^{' $O/g2.log
 timeout -k 10 400 python3 -u bench.py --gpus 2 --backend gloo --steps 4 --rho 1.02 --check on > $O/g2_bad.log 2>&1
 r=$?; echo "perturbed rho rc=$r (expect non-zero)"
 grep "checks" $O/g2_bad.log | tail -2
-echo done
+echo done1
+# lane-group phase profile (IPM_PROF) at the 8,192 share
+for L in 8 16 4; do
+  timeout -k 10 200 python3 -u tools/ipm_prof.py 8192 $L > $O/prof_8192_L$L.log 2>&1 || { echo "prof L=$L rc=$?"; tail -20 $O/prof_8192_L$L.log; exit 1; }
+  tail -1 $O/prof_8192_L$L.log
+done
+timeout -k 10 200 python3 -u tools/ipm_prof.py 8192 8 --prof 0 > $O/prof_8192_L8_off.log 2>&1 && tail -1 $O/prof_8192_L8_off.log
+echo done2

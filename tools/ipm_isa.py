@@ -20,6 +20,7 @@ ap.add_argument("--model", default="farmer")
 ap.add_argument("--cm", type=int, default=1)
 ap.add_argument("--maxilp", action="store_true")
 ap.add_argument("-D", action="append", default=[])
+ap.add_argument("--wpe", type=int, default=0, help="lane-group kernel: waves per SIMD budget (ML_WPE)")
 a = ap.parse_args()
 import mpisppy_amd._lib as L  # noqa: E402
 if a.model == "farmer":
@@ -32,6 +33,12 @@ else:
     bf = [4, 32, 64] if a.S == 8192 else [32, 32, 64]
     b = aircond.batch_creator(aircond.scenario_names_creator(int(np.prod(bf))), branching_factors=bf, **AIRCOND_KW)
 src, _ = L.ipm_source(b, a.lanes)
+if a.wpe:
+    a.D.append(f"ML_WPE={a.wpe}")
+    if "ML_WPE" not in src:  # a library built before the knob: patch the kernel header
+        src = src.replace("extern \"C\" __global__ void __launch_bounds__(256) k_solve_ipm_ml",
+                          "extern \"C\" __global__ void __launch_bounds__(256) "
+                          "__attribute__((amdgpu_waves_per_eu(ML_WPE, ML_WPE))) k_solve_ipm_ml")
 defs = "".join(f"#define {d.split('=')[0]} {d.split('=', 1)[1] if '=' in d else 1}\n" for d in a.D)
 open(a.out + ".hip", "w").write("#include <hip/hip_runtime.h>\n" + defs + src)
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", "-o",
