@@ -342,7 +342,9 @@ int phgpu_ipm_info(phgpu_handle h, double* info);
 /* Diagnostics (no reference counterpart): the per-phase shader-clock cycle sums of the
  * lane-group interior point's iteration loop, out[16] -- out[0..7] phases (slacks / mu,
  * A x and A'y, KKT test, normal-equation assembly, factorisation, right-hand side + solve,
- * dx / dw, step lengths + update), out[14] waves, out[15] loop trips -- accumulated by
+ * dx / dw, step lengths + update), out[8] / out[9] the loops' shader-clock / 100 MHz
+ * real-time ticks, out[10] / out[11] the same from wave entry to the loop, out[12] / out[13]
+ * the same from wave entry to exit, out[14] waves, out[15] loop trips -- accumulated by
  * modules compiled with IPM_PROF=1 (PHGPU_IPM_DEFS) and zero otherwise; synchronises the
  * device; reset != 0 clears them. */
 int phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int reset);

@@ -70,6 +70,11 @@ def main():
         out["trips_per_wave"] = trips / max(1, p[14])
         out["cycles_per_trip"] = {k: round(v, 1) for k, v in zip(PHASES, per)}
         out["cycles_per_trip_total"] = round(sum(per), 1)
+        w = max(1, p[14])
+        out["per_wave_mean"] = {"loop_clk": p[8] / w, "loop_us_rt": p[9] / w / 100.0,
+                                "pre_loop_clk": p[10] / w, "pre_loop_us_rt": p[11] / w / 100.0,
+                                "life_clk": p[12] / w, "life_us_rt": p[13] / w / 100.0}
+        out["clock_GHz_est"] = (p[8] / max(1, p[9])) * 0.1
     print(json.dumps(out), flush=True)
 
 
