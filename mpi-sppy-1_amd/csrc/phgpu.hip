@@ -1954,9 +1954,9 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         if (h->ipm_nf > 0 || h->ipm_wave > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 6);
-            ALLOC(h->ipm_stats, 16 + 16);  // two parities of 8 statistics + the IPM_PROF sums
+            ALLOC(h->ipm_stats, 16 + 32);  // two parities of 8 statistics + the IPM_PROF sums
             if (hipMemset(h->ipm_cnt, 0, 6 * sizeof(int32_t)) != hipSuccess ||
-                hipMemset(h->ipm_stats, 0, 32 * sizeof(unsigned long long)) != hipSuccess) {
+                hipMemset(h->ipm_stats, 0, 48 * sizeof(unsigned long long)) != hipSuccess) {
                 phgpu_destroy(h);
                 return set_err(-2, "hipMemset failed");
             }
@@ -3174,9 +3174,9 @@ extern "C" int phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int reset
     if (!h || !out) return set_err(-1, "null argument");
     if (!h->ipm_stats) return set_err(-1, "no path-6 state on this handle");
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out, h->ipm_stats + 16, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(out, h->ipm_stats + 16, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return set_err(-2, "phgpu_ipm_prof: copy failed");
-    if (reset && hipMemset(h->ipm_stats + 16, 0, 16 * sizeof(unsigned long long)) != hipSuccess)
+    if (reset && hipMemset(h->ipm_stats + 16, 0, 32 * sizeof(unsigned long long)) != hipSuccess)
         return set_err(-2, "phgpu_ipm_prof: reset failed");
     return 0;
 }

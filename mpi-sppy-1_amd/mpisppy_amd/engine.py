@@ -241,7 +241,7 @@ class PHEngine:
     def ipm_prof(self, reset=True):
         """Phase cycle sums of the lane-group interior point (diagnostics; modules built with
         IPM_PROF=1 in PHGPU_IPM_DEFS, else zeros): phgpu_ipm_prof."""
-        out = (ctypes.c_ulonglong * 16)()
+        out = (ctypes.c_ulonglong * 32)()
         _lib.check(self.lib.phgpu_ipm_prof(self.h, out, 1 if reset else 0), "phgpu_ipm_prof")
         return list(out)
 

@@ -61,19 +61,22 @@ def main():
     ap.add_argument("--prof", type=int, default=1)
     a = ap.parse_args()
     dt, p, info = run(a.S, a.L, a.iters, a.defs, a.prof)
+    L = a.L
     out = {"S": a.S, "L": a.L, "ms_per_step": 1e3 * dt, "lanes": info["lanes"], "kernel": info["kernel"],
            "scratch": info["scratch_bytes"], "defs": a.defs, "prof": bool(a.prof)}
-    if a.prof and p[15]:
+    if a.prof and p[14]:
+        w = max(1, p[14])
+        us = lambda k: round(p[k] / w / 100.0, 2)  # noqa: E731  (100 MHz real-time ticks)
+        out["wave_us_mean"] = {"entry_to_loop": us(11), "loop": us(9), "loop_end_to_stores": us(16),
+                               "stats": us(17), "to_exit": us(18), "life": us(13)}
+        out["waves"] = p[14]
+        out["wave_us_max"] = {"life": p[20] / 100.0, "entry_to_loop_end": p[21] / 100.0}
+    if a.prof and p[15] and L > 1:
         trips = p[15]
         per = [v / trips for v in p[:8]]
-        out["waves"] = p[14]
         out["trips_per_wave"] = trips / max(1, p[14])
         out["cycles_per_trip"] = {k: round(v, 1) for k, v in zip(PHASES, per)}
         out["cycles_per_trip_total"] = round(sum(per), 1)
-        w = max(1, p[14])
-        out["per_wave_mean"] = {"loop_clk": p[8] / w, "loop_us_rt": p[9] / w / 100.0,
-                                "pre_loop_clk": p[10] / w, "pre_loop_us_rt": p[11] / w / 100.0,
-                                "life_clk": p[12] / w, "life_us_rt": p[13] / w / 100.0}
         out["clock_GHz_est"] = (p[8] / max(1, p[9])) * 0.1
     print(json.dumps(out), flush=True)
 
