@@ -339,17 +339,14 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
  * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
-/* Diagnostics (no reference counterpart): timing sums of the interior-point kernels' waves,
- * out[32], accumulated by modules compiled with IPM_PROF=1 (PHGPU_IPM_DEFS) and zero
- * otherwise.  Lane groups: out[0..7] shader-clock cycles of the loop's phases (slacks / mu,
- * A x and A'y, KKT test, normal-equation assembly, factorisation, right-hand side + solve,
- * dx / dw, step lengths + update), out[8] / out[9] the loop in shader clocks / 100 MHz
- * real-time ticks, out[10] / out[11] entry to loop, out[12] / out[13] entry to exit; both
- * kernels: out[9], out[11], out[13], out[14] waves, out[15] loop trips (one lane: iterations
- * of lane 0), out[16] loop end to stores done, out[17] statistics (lane groups), out[18]
- * to exit, out[20] / out[21] the maxima over waves of entry to exit / entry to loop end
- * (real-time ticks).  Synchronises the device; reset != 0 clears them. */
-int phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int reset);
+/* Diagnostics (no reference counterpart): the per-wave timelines of the last path-6 launch,
+ * stored by modules compiled with IPM_PROF=1 (PHGPU_IPM_DEFS) on a handle created with
+ * PHGPU_IPM_PROF=1 in the environment: 16 words per wave (wave = block * 4 + wave in block):
+ * 100 MHz real-time stamps at entry, loop start, loop end, stores done, statistics done and
+ * exit, the loop trips, and with IPM_PROF=2 (lane groups) words 8..15 the shader-clock
+ * cycles of the loop's phases.  Copies min(n, available) words to out (synchronising the
+ * device) and returns the words available (0: no buffer), < 0 on error. */
+int64_t phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int64_t n);
 
 /* The path-6 source the library generates for a pattern and its data flags (host code
  * only; tests and tools).  flags / v0 are per element of [A nnz | c n | q n | lb n | ub n |

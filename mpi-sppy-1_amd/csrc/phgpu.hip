@@ -175,6 +175,8 @@ struct phgpu_state {
     // status / iters outputs into stats_gen[8].  last_stats: where the last solve's are
     // (null: compute on request)
     unsigned long long *ipm_stats, *stats_gen, *last_stats;
+    unsigned long long* ipm_prof;  // PHGPU_IPM_PROF: per-wave timelines of IPM_PROF modules
+    long long ipm_prof_n;
     const int32_t *last_status, *last_iters;
     // x̄ partial sums written by the path-6 kernels' epilogue, per warm slot:
     // [chunks * nn * 2] sums of pcoef x and pcoef x^2, node tags [chunks * nn], fallback
@@ -1954,9 +1956,13 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         if (h->ipm_nf > 0 || h->ipm_wave > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 6);
-            ALLOC(h->ipm_stats, 16 + 32);  // two parities of 8 statistics + the IPM_PROF sums
+            ALLOC(h->ipm_stats, 16);
+            if (getenv("PHGPU_IPM_PROF")) {  // diagnostics: 16 words per wave of the widest plan
+                h->ipm_prof_n = 16 * ((Sz * 64 + 63) / 64 + 64);
+                ALLOC(h->ipm_prof, h->ipm_prof_n);
+            }
             if (hipMemset(h->ipm_cnt, 0, 6 * sizeof(int32_t)) != hipSuccess ||
-                hipMemset(h->ipm_stats, 0, 48 * sizeof(unsigned long long)) != hipSuccess) {
+                hipMemset(h->ipm_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
                 phgpu_destroy(h);
                 return set_err(-2, "hipMemset failed");
             }
@@ -3110,6 +3116,7 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
     if (h->ipm_list) (void)hipFree(h->ipm_list);
     if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
     if (h->ipm_stats) (void)hipFree(h->ipm_stats);
+    if (h->ipm_prof) (void)hipFree(h->ipm_prof);
     if (h->stats_gen) (void)hipFree(h->stats_gen);
     {
         void* more[] = {h->xp[0], h->xp[1], h->xp_node[0], h->xp_node[1], h->xp_dirty[0], h->xp_dirty[1],
@@ -3170,15 +3177,15 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     return 0;
 }
 
-extern "C" int phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int reset) {
-    if (!h || !out) return set_err(-1, "null argument");
-    if (!h->ipm_stats) return set_err(-1, "no path-6 state on this handle");
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out, h->ipm_stats + 16, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+extern "C" long long phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, long long n) {
+    if (!h) return set_err(-1, "null handle");
+    if (!h->ipm_prof) return 0;
+    const long long k = n < h->ipm_prof_n ? n : h->ipm_prof_n;
+    if (out && k > 0 &&
+        (hipDeviceSynchronize() != hipSuccess ||
+         hipMemcpy(out, h->ipm_prof, k * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess))
         return set_err(-2, "phgpu_ipm_prof: copy failed");
-    if (reset && hipMemset(h->ipm_stats + 16, 0, 32 * sizeof(unsigned long long)) != hipSuccess)
-        return set_err(-2, "phgpu_ipm_prof: reset failed");
-    return 0;
+    return h->ipm_prof_n;
 }
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {

@@ -96,12 +96,13 @@ def load(path=None):
     lib.phgpu_workspace_bytes.restype = c_i64
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
-    lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_int]
+    lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_i64]
+    lib.phgpu_ipm_prof.restype = c_i64
     lib.phgpu_solve_stats.argtypes = [c_vp, c_vp, c_vp]
     lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl), c_i32,
                                      ctypes.c_char_p, ctypes.c_size_t, P_i32]
     for name in EXPORTS:
-        if name != "phgpu_workspace_bytes":
+        if name not in ("phgpu_workspace_bytes", "phgpu_ipm_prof"):
             getattr(lib, name).restype = c_int
     if path is None:
         _lib = lib

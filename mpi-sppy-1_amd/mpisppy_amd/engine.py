@@ -238,12 +238,20 @@ class PHEngine:
                 "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel", "jam_handovers", "recentrings"]
         return dict(zip(keys, list(info)))
 
-    def ipm_prof(self, reset=True):
-        """Phase cycle sums of the lane-group interior point (diagnostics; modules built with
-        IPM_PROF=1 in PHGPU_IPM_DEFS, else zeros): phgpu_ipm_prof."""
-        out = (ctypes.c_ulonglong * 32)()
-        _lib.check(self.lib.phgpu_ipm_prof(self.h, out, 1 if reset else 0), "phgpu_ipm_prof")
-        return list(out)
+    def ipm_prof(self):
+        """Per-wave timelines of the last path-6 launch (diagnostics; modules built with
+        IPM_PROF in PHGPU_IPM_DEFS on a handle created with PHGPU_IPM_PROF=1): an
+        [waves, 16] uint64 array (phgpu_ipm_prof), or None without the buffer."""
+        n = int(self.lib.phgpu_ipm_prof(self.h, None, 0))
+        if n < 0:
+            _lib.check(-1, "phgpu_ipm_prof")
+        if n == 0:
+            return None
+        out = np.zeros(n, dtype=np.uint64)
+        rc = int(self.lib.phgpu_ipm_prof(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), n))
+        if rc < 0:
+            _lib.check(rc, "phgpu_ipm_prof")
+        return out.reshape(-1, 16)
 
     # -------------------------------------------------------------- PH state
     def set_rho(self, rho):

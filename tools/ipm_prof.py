@@ -20,9 +20,11 @@ sys.path.insert(0, ROOT)
 PHASES = ["slacks+mu", "Ax+Aty+pq", "kkt", "assembly", "factor", "rhs+solve", "dx+dw", "step+update"]
 
 
-def run(S, L, iters, defs, prof):
+def run(S, L, iters, defs, prof, level=1):
     os.environ["PHGPU_IPM_LANES"] = str(L)
-    d = (defs + ";" if defs else "") + ("IPM_PROF=1" if prof else "")
+    if prof:
+        os.environ["PHGPU_IPM_PROF"] = "1"
+    d = (defs + ";" if defs else "") + (f"IPM_PROF={level}" if prof else "")
     if d:
         os.environ["PHGPU_IPM_DEFS"] = d
     else:
@@ -40,14 +42,13 @@ def run(S, L, iters, defs, prof):
     ph.iterk_loop()
     e = ph.engine
     info = e.ipm_info()
-    e.ipm_prof(reset=True)
     ph.options["PHIterLimit"] = iters
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ph.iterk_loop()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
-    p = e.ipm_prof(reset=True)
+    p = e.ipm_prof() if prof else None
     e.close()
     return dt, p, info
 
@@ -59,25 +60,35 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--defs", default="")
     ap.add_argument("--prof", type=int, default=1)
+    ap.add_argument("--level", type=int, default=1)
     a = ap.parse_args()
-    dt, p, info = run(a.S, a.L, a.iters, a.defs, a.prof)
-    L = a.L
+    dt, p, info = run(a.S, a.L, a.iters, a.defs, a.prof, a.level)
     out = {"S": a.S, "L": a.L, "ms_per_step": 1e3 * dt, "lanes": info["lanes"], "kernel": info["kernel"],
            "scratch": info["scratch_bytes"], "defs": a.defs, "prof": bool(a.prof)}
-    if a.prof and p[14]:
-        w = max(1, p[14])
-        us = lambda k: round(p[k] / w / 100.0, 2)  # noqa: E731  (100 MHz real-time ticks)
-        out["wave_us_mean"] = {"entry_to_loop": us(11), "loop": us(9), "loop_end_to_stores": us(16),
-                               "stats": us(17), "to_exit": us(18), "life": us(13)}
-        out["waves"] = p[14]
-        out["wave_us_max"] = {"life": p[20] / 100.0, "entry_to_loop_end": p[21] / 100.0}
-    if a.prof and p[15] and L > 1:
-        trips = p[15]
-        per = [v / trips for v in p[:8]]
-        out["trips_per_wave"] = trips / max(1, p[14])
-        out["cycles_per_trip"] = {k: round(v, 1) for k, v in zip(PHASES, per)}
-        out["cycles_per_trip_total"] = round(sum(per), 1)
-        out["clock_GHz_est"] = (p[8] / max(1, p[9])) * 0.1
+    if p is not None:
+        import numpy as np
+        nw = int(np.ceil(a.S * max(1, int(info["lanes"])) / 64.0))
+        r = p[:nw].astype(np.float64)
+        ok = r[:, 5] > 0
+        r = r[ok]
+        t0 = r[:, 0].min()
+        us = lambda v: round(float(v) / 100.0, 2)  # noqa: E731  (100 MHz ticks)
+        seg = {"entry_delay": r[:, 0] - t0, "pre_loop": r[:, 1] - r[:, 0], "loop": r[:, 2] - r[:, 1],
+               "stores": r[:, 3] - r[:, 2], "stats": r[:, 4] - r[:, 3], "epilogue": r[:, 5] - r[:, 4],
+               "life": r[:, 5] - r[:, 0]}
+        out["waves"] = int(ok.sum())
+        out["span_us"] = us(r[:, 5].max() - t0)
+        out["seg_mean_us"] = {k: us(v.mean()) for k, v in seg.items()}
+        out["seg_max_us"] = {k: us(v.max()) for k, v in seg.items()}
+        crit = int(np.argmax(r[:, 5]))
+        out["critical_wave"] = {"wave": crit, "trips": int(r[crit, 6]), **{k: us(v[crit]) for k, v in seg.items()}}
+        out["trips"] = {"mean": float(r[:, 6].mean()), "max": int(r[:, 6].max())}
+        loop_per_trip = seg["loop"] / np.maximum(r[:, 6], 1)
+        out["loop_us_per_trip"] = {"mean": us(loop_per_trip.mean()), "max": us(loop_per_trip.max())}
+        if a.level >= 2 and a.L > 1:
+            tr = r[:, 6].sum()
+            per = r[:, 8:16].sum(0) / max(1.0, tr)
+            out["cycles_per_trip"] = {k: round(float(v), 1) for k, v in zip(PHASES, per)}
     print(json.dumps(out), flush=True)
 
 
