@@ -3177,10 +3177,10 @@ extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     return 0;
 }
 
-extern "C" long long phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, long long n) {
+extern "C" int64_t phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int64_t n) {
     if (!h) return set_err(-1, "null handle");
     if (!h->ipm_prof) return 0;
-    const long long k = n < h->ipm_prof_n ? n : h->ipm_prof_n;
+    const int64_t k = n < h->ipm_prof_n ? n : h->ipm_prof_n;
     if (out && k > 0 &&
         (hipDeviceSynchronize() != hipSuccess ||
          hipMemcpy(out, h->ipm_prof, k * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess))
