@@ -174,6 +174,8 @@ struct phgpu_state {
     // parity, [2][8]); other paths get them from k_solve_stats over the last solve's
     // status / iters outputs into stats_gen[8].  last_stats: where the last solve's are
     // (null: compute on request)
+    // ipm_stats: two parities of PHGPU_STATS_COPIES copies of the 8 statistics words (the
+    // path-6 kernels spread their per-wave atomics over the copies, stats_word sums them)
     unsigned long long *ipm_stats, *stats_gen, *last_stats;
     unsigned long long* ipm_prof;  // PHGPU_IPM_PROF: per-wave timelines of IPM_PROF modules
     long long ipm_prof_n;
@@ -918,6 +920,30 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
     }
 }
 
+// The path-6 statistics {OPTIMAL, ITER_LIMIT, PRIMAL_INF, DUAL_INF, iteration sum, iteration
+// maximum, jam hand-overs, re-centrings} are PHGPU_STATS_COPIES copies, one 128-B line each:
+// wave w of a path-6 kernel adds to copy w % copies.  One copy took every wave's atomics,
+// thousands on one L2 line, serialised there for ~20 us at the end of the 8,192-share launch
+// (the stores and epilogue queued behind them; tools/ipm_prof.py).  Readers sum
+// the copies (the maximum for word 5); stats_gen (paths without in-kernel statistics) is one
+// copy.
+#define PHGPU_STATS_COPIES 32
+#define PHGPU_STATS_STRIDE 16
+#define PHGPU_STATS_WORDS (PHGPU_STATS_COPIES * PHGPU_STATS_STRIDE)
+__host__ __device__ inline unsigned long long stats_word(const unsigned long long* s, int copies, int k) {
+    unsigned long long a = 0;
+    for (int c = 0; c < copies; ++c) {
+        const unsigned long long v = s[c * PHGPU_STATS_STRIDE + k];
+        a = (k == 5) ? (v > a ? v : a) : a + v;
+    }
+    return a;
+}
+
+// the six statistics of a solve into out (int64), one thread (the update kernels' sinks)
+__global__ void k_stats_copy(const unsigned long long* __restrict__ src, int copies, int64_t* __restrict__ out) {
+    if (threadIdx.x < 6) out[threadIdx.x] = (int64_t)stats_word(src, copies, threadIdx.x);
+}
+
 #include "solve_reg.inc"
 #include "solve_wg.inc"
 #include "solve_stream.inc"
@@ -1134,6 +1160,7 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
 struct conv_sink {
     double* conv;                          // conv_local (pinned host or device memory)
     const unsigned long long* stats_src;   // the last solve's statistics (device), or null
+    int stats_copies;                      // copies of them at stats_src (stats_word)
     int64_t* stats_dst;                    // where they go (pinned host or device), or null
     double scale;                          // 1 / (S nn)
     double* cpart;                         // [gridDim.x] block partials
@@ -1186,7 +1213,8 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
     if (threadIdx.x < WAVE) {
         double t = 0.0;
         for (int u = 0; u < nwb; ++u) t += red[u];
-        if (threadIdx.x < 6 && o.stats_dst) o.stats_dst[threadIdx.x] = (int64_t)o.stats_src[threadIdx.x];
+        if (threadIdx.x < 6 && o.stats_dst)
+            o.stats_dst[threadIdx.x] = (int64_t)stats_word(o.stats_src, o.stats_copies, threadIdx.x);
         if (threadIdx.x == 6) *o.conv = t * o.scale;
         if (threadIdx.x == 0) __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1353,7 +1381,7 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__
                                                      int64_t* __restrict__ stats_dst = nullptr) {
     __shared__ double sh[256];
     const int k = blockIdx.x;
-    if (stats_dst && k == 0 && threadIdx.x < 6) stats_dst[threadIdx.x] = (int64_t)stats_src[threadIdx.x];
+    if (stats_dst && k == 0 && threadIdx.x < 6) stats_dst[threadIdx.x] = (int64_t)stats_word(stats_src, 1, threadIdx.x);
     double a = 0.0;
     for (int64_t w = threadIdx.x; w < nw; w += 256) a += part[w * K + k];
     sh[threadIdx.x] = a;
@@ -1956,13 +1984,13 @@ extern "C" int phgpu_create2(phgpu_handle* out, int device, int64_t S, int32_t n
         if (h->ipm_nf > 0 || h->ipm_wave > 0) {
             ALLOC(h->ipm_list, Sz);
             ALLOC(h->ipm_cnt, 6);
-            ALLOC(h->ipm_stats, 16);
+            ALLOC(h->ipm_stats, 2 * PHGPU_STATS_WORDS);
             if (getenv("PHGPU_IPM_PROF")) {  // diagnostics: 16 words per wave of the widest plan
                 h->ipm_prof_n = 16 * ((Sz * 64 + 63) / 64 + 64);
                 ALLOC(h->ipm_prof, h->ipm_prof_n);
             }
             if (hipMemset(h->ipm_cnt, 0, 6 * sizeof(int32_t)) != hipSuccess ||
-                hipMemset(h->ipm_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+                hipMemset(h->ipm_stats, 0, 2 * PHGPU_STATS_WORDS * sizeof(unsigned long long)) != hipSuccess) {
                 phgpu_destroy(h);
                 return set_err(-2, "hipMemset failed");
             }
@@ -2591,7 +2619,7 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
                           (h->ipm && (h->ipm->L == 1 || (fe && atoi(fe) == 1 && h->ipm->L < 64))) &&
                           h->nb_idx && h->xbar_single && h->xbar_mixed == 0 && h->nn > 0 && h->nn <= XL_NN_MAX &&
                           xp_valid(h, q.x) && q.W == h->W && q.xbar == h->xbar && q.rho == h->rho &&
-                          (!q.stats || (stats_keep && stats_keep == h->ipm_stats + 8 * (1 - h->ipm_parity)));
+                          (!q.stats || (stats_keep && stats_keep == h->ipm_stats + PHGPU_STATS_WORDS * (1 - h->ipm_parity)));
         if (fuse) {
             h->fuse_now = 1;
             ++h->folded;
@@ -2843,6 +2871,10 @@ extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
                            h->stats_gen);
         HIPCHK(hipGetLastError());
         src = h->stats_gen;
+    } else {  // the path-6 copies, summed into stats_gen (out may be pageable host memory)
+        hipLaunchKernelGGL(k_stats_copy, dim3(1), dim3(64), 0, st, src, PHGPU_STATS_COPIES, (int64_t*)h->stats_gen);
+        HIPCHK(hipGetLastError());
+        src = h->stats_gen;
     }
     HIPCHK(hipMemcpyAsync(out, src, 6 * sizeof(int64_t), hipMemcpyDefault, st));
     return 0;
@@ -2937,11 +2969,13 @@ static int make_sink(phgpu_state* h, double* conv_local, int64_t* stats_out, hip
     o.conv = conv_local;
     o.stats_dst = stats_out;
     o.stats_src = stats_out ? h->last_stats : nullptr;
+    o.stats_copies = PHGPU_STATS_COPIES;  // last_stats: the path-6 statistics
     if (stats_out && !o.stats_src) {  // a path without in-kernel statistics
         hipLaunchKernelGGL(k_solve_stats, dim3(1), dim3(SC_T), 0, st, h->last_status, h->last_iters, h->S,
                            h->stats_gen);
         HIPCHK(hipGetLastError());
         o.stats_src = h->stats_gen;
+        o.stats_copies = 1;
     }
     o.scale = (h->nn > 0) ? 1.0 / ((double)h->S * (double)h->nn) : 0.0;
     o.cpart = h->cpart_blk;
@@ -3208,13 +3242,14 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     }
     // the subtree kernel's jam statistics of the last path-6 solve (synchronous read)
     if (h->last_stats && h->ipm_stats && h->last_path == 6) {
-        unsigned long long st8[8];
+        std::vector<unsigned long long> st(PHGPU_STATS_WORDS);
         // the solve may still run on a non-blocking stream (a torch side stream, the
         // speculative launch), which hipMemcpy does not wait for: finish it first
         if (hipDeviceSynchronize() == hipSuccess &&
-            hipMemcpy(st8, h->last_stats, sizeof(st8), hipMemcpyDeviceToHost) == hipSuccess) {
-            info[13] = (double)st8[6];
-            info[14] = (double)st8[7];
+            hipMemcpy(st.data(), h->last_stats, PHGPU_STATS_WORDS * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost) == hipSuccess) {
+            info[13] = (double)stats_word(st.data(), PHGPU_STATS_COPIES, 6);
+            info[14] = (double)stats_word(st.data(), PHGPU_STATS_COPIES, 7);
         }
     }
     return 0;

@@ -45,6 +45,7 @@ static inline void __syncthreads() { g_bar->arrive_and_wait(); }
 static inline int atomicAdd(int* p, int v) { std::lock_guard<std::mutex> l(g_mu); int o = *p; *p += v; return o; }
 static inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) { std::lock_guard<std::mutex> l(g_mu); unsigned long long o = *p; *p += v; return o; }
 static inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) { std::lock_guard<std::mutex> l(g_mu); unsigned long long o = *p; if (v > o) *p = v; return o; }
+template <class T> static inline T __shfl_xor(T, int, int) { return T(0); }  // (ipm_stats_roll without dst only)
 static double g_post[4096];
 template <int NV> static inline void w_bmax(double (&v)[NV], double*);
 template <int NV> static inline void w_bsum(double (&v)[NV], double*) {
@@ -166,12 +167,18 @@ def solve(batch, lanes=64, W=None, rho=None, xbar=None, eps_rel=1e-9, eps_abs=1e
     p.eps_rel, p.eps_abs, p.max_ipm, p.eps_tight = eps_rel, eps_abs, max_ipm, eps_tight
     p.x_in = ptr(T(x_in)) if x_in is not None else None
     p.y_in = ptr(T(y_in)) if y_in is not None else None
-    st16 = np.zeros(16, dtype=np.uint64)
-    keep.append(st16)
-    p.stats, p.stats_zero = st16.ctypes.data, st16[8:].ctypes.data
+    # two parities of the generated IPM_SC copies of IPM_SS words (phgpu.hip stats_word)
+    sc = int(src.split("#define IPM_SC ", 1)[1].split()[0])
+    ss = int(src.split("#define IPM_SS ", 1)[1].split()[0])
+    stb = np.zeros(2 * sc * ss, dtype=np.uint64)
+    keep.append(stb)
+    p.stats, p.stats_zero = stb.ctypes.data, stb[sc * ss:].ctypes.data
     lib.wave_run(ctypes.byref(p), S)
     if stats is not None:
-        stats.append(st16[:8].copy())
+        cp = stb[:sc * ss].reshape(sc, ss)[:, :8]
+        words = cp.sum(0)
+        words[5] = cp[:, 5].max()
+        stats.append(words)
     st = status.copy()
     st[fl[:cnt[0]]] = -1
     return out["x"].T.copy(), out["y"].T.copy(), obj, bound, st, iters
