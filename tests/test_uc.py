@@ -110,3 +110,48 @@ def test_lp_optimum_vs_fixture():
         # the relaxation's commitment is mostly integral
         on = x[b.nonant_col]
         assert np.mean((on > 1e-6) & (on < 1 - 1e-6)) < 0.05
+
+
+def test_uc_ph_oracle_fixture_consistent():
+    """tests/golden/uc_ph.npz (oracle/uc_qp.py's three PH iterations on Scenario1..8): its
+    Iter0 LP objectives agree with HiGHS (uc.json) to north_star's 1e-5 relative (1.8e-6 at
+    worst: the two solvers' answers on these degenerate LPs), every solve reached a relative KKT
+    error of 2e-8, and its PH state follows the PH updates
+    (phbase.py:293-318): W_{k+1} - W_k = rho (x_k - x̄_k) sums to 0 over the scenarios."""
+    import json
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "uc_ph.npz"))
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "uc.json")))
+    assert list(d["names"]) == g["names"]
+    rel = np.abs(d["iter0_obj"] - np.array(g["lp_obj"])) / np.abs(g["lp_obj"])
+    assert rel.max() <= 1e-5, rel
+    assert d["kkt"].max() <= 2e-8 and d["iter0_kkt"].max() <= 2e-8
+    Ws = np.concatenate([d["W1"][None], d["W"]])
+    for k in range(3):
+        dW = Ws[k + 1] - Ws[k]
+        assert np.abs(dW.sum(0)).max() <= 1e-9 * max(1.0, np.abs(dW).max())
+    assert np.abs(d["W1"].sum(0)).max() <= 1e-9 * max(1.0, np.abs(d["W1"]).max())
+
+
+def test_uc_qp_oracle_matches_dense_ipm_on_random_qps():
+    """oracle/uc_qp.py (sparse Mehrotra IPM) against oracle/lpqp.py's dense IPM on small
+    random LP / QP batches with every row and bound kind."""
+    from oracle.lpqp import solve_qp_ipm
+    from oracle.uc_qp import solve_qp
+    rng = np.random.default_rng(0)
+    for trial in range(5):
+        m, n = 8, 12
+        A = rng.standard_normal((m, n)) * (rng.random((m, n)) < 0.5)
+        x0 = rng.random(n)
+        ax = A @ x0
+        rl, ru = ax - rng.random(m), ax + rng.random(m)
+        rl[:2] = ru[:2] = ax[:2]
+        rl[2] = -np.inf
+        lb, ub = np.zeros(n), np.full(n, 2.0)
+        ub[3], lb[4] = np.inf, -np.inf
+        c = rng.standard_normal(n)
+        q = np.where(rng.random(n) < 0.5, rng.random(n), 0.0)
+        r = solve_qp(A, rl, ru, lb, ub, c, q)
+        xr, ob, st = solve_qp_ipm(A, rl, ru, lb, ub, c, q)
+        assert r["status"] == 0 and st == 0
+        assert abs(r["obj"] - ob) <= 1e-8 * (1 + abs(ob)), (trial, r["obj"], ob)
+        assert np.abs(r["x"] - xr).max() <= 1e-6, trial
