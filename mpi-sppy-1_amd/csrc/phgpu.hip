@@ -930,7 +930,7 @@ k_solve(phgpu_state st, solve_params P, double* __restrict__ xout, double* __res
 #define PHGPU_STATS_COPIES 32
 #define PHGPU_STATS_STRIDE 16
 #define PHGPU_STATS_WORDS (PHGPU_STATS_COPIES * PHGPU_STATS_STRIDE)
-__host__ __device__ inline unsigned long long stats_word(const unsigned long long* s, int copies, int k) {
+inline unsigned long long stats_word(const unsigned long long* s, int copies, int k) {
     unsigned long long a = 0;
     for (int c = 0; c < copies; ++c) {
         const unsigned long long v = s[c * PHGPU_STATS_STRIDE + k];
@@ -939,9 +939,33 @@ __host__ __device__ inline unsigned long long stats_word(const unsigned long lon
     return a;
 }
 
-// the six statistics of a solve into out (int64), one thread (the update kernels' sinks)
+// the six statistics summed over the copies by a whole wave: lane t < copies reads copy t (one
+// load latency; a thread reading the 32 copies in turn took 8 us), the wave reduces, every
+// lane returns them
+__device__ __forceinline__ void stats_wave(const unsigned long long* __restrict__ s, int copies,
+                                           unsigned long long v[6]) {
+    const int t = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = t < copies ? s[t * PHGPU_STATS_STRIDE + k] : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const unsigned long long u = __shfl_xor(v[k], o, 64);
+            v[k] = k == 5 ? (u > v[k] ? u : v[k]) : v[k] + u;
+        }
+}
+
+// the six statistics of a solve into out (int64): one wave
 __global__ void k_stats_copy(const unsigned long long* __restrict__ src, int copies, int64_t* __restrict__ out) {
-    if (threadIdx.x < 6) out[threadIdx.x] = (int64_t)stats_word(src, copies, threadIdx.x);
+    unsigned long long v[6];
+    stats_wave(src, copies, v);
+    if (threadIdx.x < 6) {
+        unsigned long long w = v[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k) w = (int)threadIdx.x == k ? v[k] : w;
+        out[threadIdx.x] = (int64_t)w;
+    }
 }
 
 #include "solve_reg.inc"
@@ -1213,8 +1237,14 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
     if (threadIdx.x < WAVE) {
         double t = 0.0;
         for (int u = 0; u < nwb; ++u) t += red[u];
-        if (threadIdx.x < 6 && o.stats_dst)
-            o.stats_dst[threadIdx.x] = (int64_t)stats_word(o.stats_src, o.stats_copies, threadIdx.x);
+        if (o.stats_dst) {
+            unsigned long long v[6];
+            stats_wave(o.stats_src, o.stats_copies, v);
+            unsigned long long w = v[0];
+#pragma unroll
+            for (int k = 1; k < 6; ++k) w = (int)threadIdx.x == k ? v[k] : w;
+            if (threadIdx.x < 6) o.stats_dst[threadIdx.x] = (int64_t)w;
+        }
         if (threadIdx.x == 6) *o.conv = t * o.scale;
         if (threadIdx.x == 0) __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1381,7 +1411,7 @@ __global__ void __launch_bounds__(256) k_sum_partials(const double* __restrict__
                                                      int64_t* __restrict__ stats_dst = nullptr) {
     __shared__ double sh[256];
     const int k = blockIdx.x;
-    if (stats_dst && k == 0 && threadIdx.x < 6) stats_dst[threadIdx.x] = (int64_t)stats_word(stats_src, 1, threadIdx.x);
+    if (stats_dst && k == 0 && threadIdx.x < 6) stats_dst[threadIdx.x] = (int64_t)stats_src[threadIdx.x];  // (one copy)
     double a = 0.0;
     for (int64_t w = threadIdx.x; w < nw; w += 256) a += part[w * K + k];
     sh[threadIdx.x] = a;

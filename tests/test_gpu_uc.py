@@ -237,14 +237,18 @@ def test_path4_split_matches_queue_on_aircond(gpu):
 
 
 @pytest.mark.timeout(900)
-def test_uc_ph_subproblems_vs_cpu_interior_point(gpu):
+@pytest.mark.parametrize("eps,obj_rel", [(UC_EPS, 5e-5), (2e-7, UC_OBJ_REL)])
+def test_uc_ph_subproblems_vs_cpu_interior_point(gpu, eps, obj_rel):
     """Config 5's PH subproblems against an independent second-order solve:
     tests/golden/uc_ph.npz holds three PH iterations on Scenario1..8 solved by the sparse
     Mehrotra interior point of oracle/uc_qp.py (make_golden_uc_ph.py).  Each iteration installs
     the oracle's PH state (W_k, x̄_{k-1}) on the GPU engine, solves all 8 QPs on path 4 at
     config 5's eps_rel 1e-6, and compares:
 
-      * the augmented PH objective of every QP: 1e-5 relative (north_star's objective bar);
+      * the augmented PH objective of every QP: north_star's 1e-5 relative with the QPs
+        solved to eps_rel 2e-7; at config 5's own eps_rel 1e-6 within 5e-5 (the relative KKT
+        test bounds the primal residual by eps (1 + ||b||), and UC's loads put ||b|| at
+        ~1e4: 3.4e-5 measured on Scenario5 of the first PH iteration);
       * x̄_k and conv: 0.05 absolute.  UC's nonants are not pinned finer by either solver:
         uc_funcs.py's rho spans 1e-4 .. 11.6, and a nonant's distance to the QP optimum is
         bounded by sqrt(2 gap / rho) -- at rho = 1e-4 a gap of 1e-6 of the objective leaves
@@ -268,7 +272,7 @@ def test_uc_ph_subproblems_vs_cpu_interior_point(gpu):
     xbs = [d["xbar0"], d["xbar"][0], d["xbar"][1]]
     nc = np.asarray(b.nonant_col)
     opts = dict(uc.PDHG_ITERK_OPTIONS)
-    opts["eps_rel"] = UC_EPS
+    opts["eps_rel"] = eps
     for k in range(3):
         e.set_W(Ws[k])
         e.set_xbar(np.tile(xbs[k], (S, 1)))
@@ -278,7 +282,7 @@ def test_uc_ph_subproblems_vs_cpu_interior_point(gpu):
         obj = e.host("obj")
         want = d["obj"][k]
         rel = np.abs(obj - want) / np.abs(want)
-        assert rel.max() <= UC_OBJ_REL, (k, rel.max(), obj, want)
+        assert rel.max() <= obj_rel, (k, rel.max(), obj, want)
         x = e.host("x")[:, nc]
         xb = x.mean(0)
         assert np.abs(xb - d["xbar"][k]).max() <= 0.05, (k, np.abs(xb - d["xbar"][k]).max())
