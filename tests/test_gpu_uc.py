@@ -249,12 +249,12 @@ def test_uc_ph_subproblems_vs_cpu_interior_point(gpu, eps, obj_rel):
         solved to eps_rel 2e-7; at config 5's own eps_rel 1e-6 within 5e-5 (the relative KKT
         test bounds the primal residual by eps (1 + ||b||), and UC's loads put ||b|| at
         ~1e4: 3.4e-5 measured on Scenario5 of the first PH iteration);
-      * x̄_k and conv: 0.05 absolute.  UC's nonants are not pinned finer by either solver:
-        uc_funcs.py's rho spans 1e-4 .. 11.6, and a nonant's distance to the QP optimum is
+      * the nonants in the rho-weighted norm the proximal term makes the QP strongly convex
+        in: within twice sqrt(2 (objective gap)).  A per-nonant comparison is not well posed:
+        uc_funcs.py's rho spans 1e-4 .. 11.6 and a nonant's distance to the optimum is only
         bounded by sqrt(2 gap / rho) -- at rho = 1e-4 a gap of 1e-6 of the objective leaves
-        it free across [0, 1].  The oracle's own nonants move by 2.3e-2 between its KKT
-        tolerances 1e-8 and 1e-10 (tests/golden/make_golden_uc_ph.py); x̄, a mean over 8
-        scenarios, is compared at twice that.
+        it free across [0, 1] (the oracle's own nonants move by 2.3e-2 between its KKT
+        tolerances 1e-8 and 1e-10; x̄ of the GPU differed from the oracle's by 0.12 at eps 1e-6).
 
     Parity stays UNPINNED against the reference (it ships no UC output)."""
     from mpisppy_amd import _lib
@@ -283,9 +283,14 @@ def test_uc_ph_subproblems_vs_cpu_interior_point(gpu, eps, obj_rel):
         want = d["obj"][k]
         rel = np.abs(obj - want) / np.abs(want)
         assert rel.max() <= obj_rel, (k, rel.max(), obj, want)
+        # the oracle's nonants of this iteration from its PH state: x_k = (W_{k+1} - W_k) / rho + x̄_k
         x = e.host("x")[:, nc]
-        xb = x.mean(0)
-        assert np.abs(xb - d["xbar"][k]).max() <= 0.05, (k, np.abs(xb - d["xbar"][k]).max())
-        conv = np.abs(x - xb).mean()
-        assert abs(conv - d["conv"][k]) <= 0.05, (k, conv, d["conv"][k])
+        xo = (d["W"][k] - Ws[k]) / d["rho"] + d["xbar"][k]
+        # strong convexity in the rho-norm: f(x) - f(x*) >= 1/2 ||x_N - x*_N||_rho^2, so two
+        # solutions whose objectives agree to dobj sit within sqrt(2 (dobj_gpu + dobj_oracle))
+        # of the optimum's nonants; dobj from the measured objective gap plus the oracle's
+        # own 2e-6 relative (its LP objectives against HiGHS, test_uc.py)
+        dist = np.sqrt((d["rho"] * (x - xo) ** 2).sum(1))
+        bound = np.sqrt(2.0 * (np.abs(obj - want) + 2e-6 * np.abs(want))) * 2.0
+        assert (dist <= bound).all(), (k, dist, bound)
     e.close()
