@@ -71,6 +71,9 @@ def parse():
                         "farmer 1,024 cm=10, aircond 32x32x64) and exit non-zero on a mismatch; auto: when "
                         "the workload and rho match a fixture, on: whenever the workload has one (a "
                         "different --rho then fails by design)")
+    p.add_argument("--no-fused-loop", action="store_true",
+                   help="one rank: run PHBase.iterk_loop step by step instead of the fused loop launch "
+                        "(the comparison case)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     p.add_argument("--profile-dir", default=None,
@@ -585,7 +588,7 @@ def main():
     comm = Comm()
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": a.warmup, "defaultPHrho": a.rho,
             "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
-            "device": f"cuda:{dev_index}",
+            "device": f"cuda:{dev_index}", "fused_ph_loop": not a.no_fused_loop,
             "iterk_solver_options": {"eps_rel": a.eps}}
     if a.model == "farmer" and not a.default_solver_options:
         # the example's recommended PH-solve options (examples/farmer.py PDHG_ITERK_OPTIONS)
@@ -663,8 +666,11 @@ def main():
             _wait, _diff = e.convergence_wait, e.convergence_diff
             e.convergence_wait = lambda: conv_seen.append(_wait()) or conv_seen[-1]
             e.convergence_diff = lambda: conv_seen.append(_diff()) or conv_seen[-1]
+        nf0 = len(getattr(ph, "fused_loops", []))
         ph.iterk_loop()                                # W warmup iterations (untimed)
         torch.cuda.synchronize()
+        if len(getattr(ph, "fused_loops", [])) > nf0:
+            conv_seen = list(ph.fused_loops[-1]["conv"])   # the fused loop's conv of every step
         checks = None
         if fixture is not None:
             del e.convergence_wait, e.convergence_diff     # back to the class methods
@@ -697,15 +703,25 @@ def main():
         ph.options["PHIterLimit"] = a.steps
         comm.Barrier()
         torch.cuda.synchronize()
+        nf0 = len(getattr(ph, "fused_loops", []))
         t0 = time.perf_counter()
         ph.iterk_loop()                                # the product loop, K iterations
         torch.cuda.synchronize()
         comm.Barrier()
         elapsed = time.perf_counter() - t0
-    launches = e.instrumented()
-    n_ins = (a.steps + INSTRUMENT_EVERY - 1) // INSTRUMENT_EVERY
-    assert len(launches) == n_ins, (len(launches), n_ins)
-    bad_timed = torch.tensor(e.instrumented_not_optimal(), dtype=torch.float64, device=e.device)
+    fused = getattr(ph, "fused_loops", [])[nf0:]
+    if fused:
+        # the fused PH loop (one launch for the K iterations): its HIP-event
+        # time per PH iteration and its IPM iterations per PH iteration
+        r = fused[-1]
+        launches = [(r["ms"] / max(1, r["steps"]), r["ipm_iters"] / max(1, r["steps"]))]
+        n_ins = 1
+        bad_timed = torch.tensor([e.count_not_optimal()], dtype=torch.float64, device=e.device)
+    else:
+        launches = e.instrumented()
+        n_ins = (a.steps + INSTRUMENT_EVERY - 1) // INSTRUMENT_EVERY
+        assert len(launches) == n_ins, (len(launches), n_ins)
+        bad_timed = torch.tensor(e.instrumented_not_optimal(), dtype=torch.float64, device=e.device)
     comm.allreduce_sum_(bad_timed)
     ar_ms = torch.tensor([e.instrumented_allreduce_ms("critical") / a.steps,
                           e.instrumented_allreduce_ms("overlapped") / a.steps], dtype=torch.float64, device=e.device)
@@ -775,6 +791,10 @@ def main():
                               # the conv all-reduce, on a side stream under the next solve
                               "allreduce_overlapped": float(ar_ms[1].item()),
                               "rest_of_step": 1e3 * elapsed / a.steps - rl["launch_ms"] - float(ar_ms[0].item())},
+            "fused_ph_loop": ({"launches": len(fused), "ph_steps": fused[-1]["steps"], "end": fused[-1]["end"],
+                               "loop_ms": fused[-1]["ms"], "ipm_iters": fused[-1]["ipm_iters"],
+                               "note": "PHBase.iterk_loop's K iterations in one cooperative launch "
+                                       "(phgpu_ph_loop); launch_ms = loop ms / K"} if fused else None),
             "instrumented_solves": {"count": n_ins, "every": INSTRUMENT_EVERY,
                                     "note": "HIP events around every INSTRUMENT_EVERY-th timed solve launch "
                                             "(roofline launch_ms); the other timed steps carry no markers"},

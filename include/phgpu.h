@@ -339,6 +339,25 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
  * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings}. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
+/* PHBase.iterk_loop (phbase.py:875-979) of one rank in one cooperative launch (no
+ * extension, converger or spoke: the loop's only decision is conv < convthresh):
+ *   for it = 1..max_iters: x̄ = the node's pcoef-weighted mean of the last solve's nonants,
+ *   W += rho (x - x̄), conv = mean |x - x̄| (phbase.py:27-107, 293-343); stop if conv <
+ *   convthresh; solve every local scenario's PH subproblem (path 6, warm-started)
+ * with every scenario's data and iterate in registers and x̄ / conv by grid-wide steps.
+ * x / y / obj / bound / status / iters as phgpu_solve (x also gives the nonants of the solve
+ * before the loop); W and x̄ are the handle's PH state (phgpu_set_ph_state, updated in place);
+ * node_buf receives the last step's node sums.  conv_hist (host, max_iters) gets each step's
+ * conv; out (host, 4): [0] PH steps taken, [1] 0 limit / 1 conv < convthresh / 2 a solve
+ * handed scenarios to the PDHG fallback (solved after the loop; the caller continues step by
+ * step), [2] IPM iterations summed over the loop's solves.  Synchronises the stream.
+ * Returns -3 (nothing launched) when the handle's state is not one it runs: several nodes
+ * per nonant depth, variable probabilities, no prox term, a path other than the one-lane
+ * interior point, or more workgroups than fit the GPU at once. */
+int phgpu_ph_loop(phgpu_handle h, const phgpu_options* opt, int max_iters, double convthresh, double* x,
+                  double* y, double* obj, double* bound, int32_t* status, int32_t* iters, double* node_buf,
+                  double* conv_hist, int64_t* out, void* stream);
+
 /* Diagnostics (no reference counterpart): the per-wave timelines of the last path-6 launch,
  * stored by modules compiled with IPM_PROF=1 (PHGPU_IPM_DEFS) on a handle created with
  * PHGPU_IPM_PROF=1 in the environment: 16 words per wave (wave = block * 4 + wave in block):

@@ -166,6 +166,13 @@ struct phgpu_state {
     // (0: not eligible); 1 once a compiled module spilled (path 6 is then not the
     // default); the fallback list [S] and its counters {fail_n[2], qhead[2]} by parity
     ipm_module* ipm;
+    // phgpu_ph_loop: the IPM_LOOP module (built on first use from the one-lane source) and its
+    // buffers {gpart [blocks * 16], gpub [16], conv_hist [cap] | gsync [2], loop_out [2],
+    // loop_its [PHGPU_STATS_WORDS]}
+    ipm_module* ipm_loop;
+    double* loop_dbl;
+    int64_t loop_dbl_n;
+    unsigned long long* loop_cnt;
     int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity, ipm_spill1;
     int ipm_wave;  // waves per scenario of the workgroup IPMs for medium scenarios (0: not eligible;
                    // jit_ipm_blk.hip.in for block-angular patterns, else jit_ipm_wave.hip.in)
@@ -2822,6 +2829,143 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     return 0;
 }
 
+// The PH loop of one rank in one cooperative launch (include/phgpu.h, solve_ipm.inc's
+// IPM_LOOP module)
+extern "C" int phgpu_ph_loop(phgpu_handle h, const phgpu_options* opt, int max_iters, double convthresh,
+                             double* x, double* y, double* obj, double* bound, int32_t* status, int32_t* iters,
+                             double* node_buf, double* conv_hist, int64_t* out, void* stream) {
+    if (!h || !x || !obj || !bound || !status || !node_buf || !conv_hist || !out) return set_err(-1, "null argument");
+    if (max_iters < 1) return set_err(-1, "phgpu_ph_loop: max_iters must be >= 1");
+    FLUSH_STEP(h);
+    hipStream_t st = (hipStream_t)stream;
+    const int why = ph_loop_eligible(h);
+    if (why) return set_err(-3, "phgpu_ph_loop: not eligible (reason %d); run the PH steps one by one", why);
+    phgpu_options o;
+    if (opt) o = *opt;
+    else phgpu_default_options(&o);
+    if (o.kernel != 0 && o.kernel != 6) return set_err(-3, "phgpu_ph_loop: path 6 only");
+    {
+        const int rc = ipm_prepare(h, st);
+        if (rc) return rc;
+    }
+    if (h->ipm->L != 1 || h->ipm->private_bytes > ipm_spill_max()) return set_err(-3, "phgpu_ph_loop: no one-lane module");
+    {
+        const int rc = ipm_loop_prepare(h);
+        if (rc) return rc;
+    }
+    ipm_module* im = h->ipm_loop;
+    const int64_t nblk = (h->S + 255) / 256;
+    if ((int64_t)std::max(im->per_cu_ipm, 0) * h->num_cus < nblk)
+        return set_err(-3, "phgpu_ph_loop: %lld workgroups do not fit the GPU at once", (long long)nblk);
+    // buffers
+    const int64_t nd = nblk * 16 + 16 + max_iters;
+    if (h->loop_dbl_n < nd) {
+        if (h->loop_dbl) HIPCHK(hipFree(h->loop_dbl));
+        h->loop_dbl = nullptr;
+        HIPCHK(hipMalloc((void**)&h->loop_dbl, (size_t)nd * sizeof(double)));
+        h->loop_dbl_n = nd;
+    }
+    if (!h->loop_cnt) HIPCHK(hipMalloc((void**)&h->loop_cnt, (size_t)(2 + PHGPU_STATS_WORDS) * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(h->loop_cnt, 0, (size_t)(2 + PHGPU_STATS_WORDS) * sizeof(unsigned long long), st));
+    // a plain (non-deferred) solve's slot bookkeeping (solve_impl)
+    h->pending = -1;
+    h->wq = h->wslot;
+    bind_slots(h);
+    const int wq = h->wq;
+    solve_params P;
+    P.eps_rel = o.eps_rel;
+    P.eps_abs = o.eps_abs;
+    P.gamma = o.gamma;
+    P.bsuff = o.beta_sufficient;
+    P.bnec = o.beta_necessary;
+    P.bart = o.beta_artificial > 0.0 ? o.beta_artificial : 1e300;
+    P.restart_every = o.restart_every;
+    P.eta_frac = o.eta_frac;
+    P.omega0 = o.omega0;
+    P.max_iter = o.max_iter;
+    P.check_every = o.check_every;
+    P.warm = h->have_solution ? 1 : 0;
+    P.keep_omega = o.keep_omega;
+    P.infeas_start = o.infeas_start;
+    P.eps_inf = o.eps_infeas;
+    P.wmax = o.omega_clamp > 1.0 ? o.omega_clamp : 1e300;
+    P.wmin = 1.0 / P.wmax;
+    const int par = h->ipm_parity;
+    h->ipm_parity ^= 1;
+    int32_t* fail_n = h->ipm_cnt + 3 * par;
+    int32_t* qhead = h->ipm_cnt + 3 * par + 1;
+    ipm_params_host a;
+    a.A = h->A; a.c = h->c; a.q = h->q; a.lb = h->lb; a.ub = h->ub; a.rl = h->rl; a.ru = h->ru; a.objc = h->objc;
+    a.lbh = h->lbh; a.ubh = h->ubh; a.Dc = h->Dc; a.Dr = h->Dr;
+    a.W = h->W; a.rho = h->rho; a.xbar = h->xbar;
+    a.omega_in = h->omega;
+    a.omega_out = h->omega_w; a.x_w = h->xw; a.y_w = h->yw;
+    a.xout = x; a.yout = y; a.obj = obj; a.bound = bound;
+    a.status = status; a.iters = iters;
+    a.fail_list = h->ipm_list; a.fail_n = fail_n;
+    a.zero3 = h->ipm_cnt + 3 * (1 - par);
+    a.stats = h->ipm_stats + PHGPU_STATS_WORDS * par; a.stats_zero = h->ipm_stats + PHGPU_STATS_WORDS * (1 - par);
+    a.prof = nullptr;
+    a.S = h->S;
+    a.W_on = h->W_on; a.prox_on = h->prox_on;
+    a.eps_rel = P.eps_rel; a.eps_abs = P.eps_abs;
+    const char* et = getenv("PHGPU_IPM_EPS");
+    a.eps_tight = (et && atof(et) > 0.0) ? atof(et) : IPM_EPS_TIGHT;
+    a.x_in = P.warm ? h->x : nullptr;
+    a.y_in = P.warm ? h->y : nullptr;
+    const char* env = getenv("PHGPU_IPM_MAXIT");
+    a.max_ipm = (env && atoi(env) >= 0) ? atoi(env) : IPM_MAXIT;
+    a.xp = nullptr;  // (no epilogue partials: the loop ends on its own PH state)
+    a.xp_node = h->xp_node[wq];
+    a.xp_dirty = h->xp_dirty[wq];
+    a.pcoef = h->pcoef;
+    a.node_of = h->node_of;
+    a.xprev = x;
+    a.W_w = const_cast<double*>(h->W);
+    a.xbar_w = const_cast<double*>(h->xbar);
+    a.node_buf = node_buf;
+    a.nb_idx = h->nb_idx;
+    a.nb_half = (long long)h->num_nodes * h->nlen_max;
+    a.gpart = h->loop_dbl;
+    a.gpub = h->loop_dbl + nblk * 16;
+    a.conv_hist = h->loop_dbl + nblk * 16 + 16;
+    a.gsync = (unsigned*)h->loop_cnt;
+    a.loop_out = (int*)(h->loop_cnt + 1);
+    a.loop_its = h->loop_cnt + 2;
+    a.conv_scale = 1.0 / ((double)h->S * (double)h->nn);
+    a.convthresh = convthresh;
+    a.loop_K = max_iters;
+    h->xp_C[wq] = 0;
+    h->last_stats = a.stats;
+    void* args[] = {&a};
+    HIPCHK(hipModuleLaunchCooperativeKernel(im->fn_ipm, (unsigned)nblk, 1, 1, 256, 1, 1, 0, st, args));
+    {
+        const int rc = ipm_fallback_launch(h, im, P, x, y, obj, bound, status, iters, qhead, fail_n, a.stats, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipGetLastError());
+    h->last_status = status;
+    h->last_iters = iters;
+    h->have_s[wq] = 1;
+    h->warm_rec_s[wq] = 0;
+    h->last_path = 6;
+    h->wslot = wq;
+    h->wq = h->wslot;
+    bind_slots(h);
+    // the loop's record (one synchronisation: the loop is one call of the host's PH loop)
+    std::vector<unsigned long long> cnt((size_t)(2 + PHGPU_STATS_WORDS));
+    HIPCHK(hipMemcpyAsync(cnt.data(), h->loop_cnt, cnt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(conv_hist, a.conv_hist, (size_t)max_iters * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int* lo = (const int*)(cnt.data() + 1);
+    out[0] = lo[0];
+    out[1] = lo[1];
+    out[2] = (int64_t)stats_word(cnt.data() + 2, PHGPU_STATS_COPIES, 0);
+    out[3] = 0;
+    if (lo[1] == 3) return set_err(-2, "phgpu_ph_loop: a grid step timed out (the launch was not co-resident)");
+    return 0;
+}
+
 // counts[c] = number of local scenarios with status c (c = 0..3), one block
 // counts[k] = #{s : status[s] == k}: one block, four statuses per load, several loads in
 // flight per thread (a device-wide "last block" reduction needs a release fence, i.e. an
@@ -3177,6 +3321,12 @@ extern "C" int phgpu_destroy(phgpu_handle h) {
         if (h->ipm->mod) (void)hipModuleUnload(h->ipm->mod);
         delete h->ipm;
     }
+    if (h->ipm_loop) {
+        if (h->ipm_loop->mod) (void)hipModuleUnload(h->ipm_loop->mod);
+        delete h->ipm_loop;
+    }
+    if (h->loop_dbl) (void)hipFree(h->loop_dbl);
+    if (h->loop_cnt) (void)hipFree(h->loop_cnt);
     if (h->ipm_list) (void)hipFree(h->ipm_list);
     if (h->ipm_cnt) (void)hipFree(h->ipm_cnt);
     if (h->ipm_stats) (void)hipFree(h->ipm_stats);

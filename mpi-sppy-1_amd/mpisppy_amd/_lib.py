@@ -50,7 +50,8 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_fix_nonants", "phgpu_status_counts", "phgpu_destroy", "phgpu_last_error", "phgpu_workspace_bytes",
            "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats",
            "phgpu_ph_update_ex", "phgpu_ph_step_local", "phgpu_ph_step_defer", "phgpu_ph_step_flush",
-           "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning", "phgpu_ipm_prof"]
+           "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning", "phgpu_ipm_prof",
+           "phgpu_ph_loop"]
 
 _lib = None
 
@@ -99,6 +100,8 @@ def load(path=None):
     lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_i64]
     lib.phgpu_ipm_prof.restype = c_i64
     lib.phgpu_solve_stats.argtypes = [c_vp, c_vp, c_vp]
+    lib.phgpu_ph_loop.argtypes = [c_vp, ctypes.POINTER(PhgpuOptions), c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp, ctypes.POINTER(c_dbl), ctypes.POINTER(c_i64), c_vp]
     lib.phgpu_ipm_source.argtypes = [c_i32, c_i32, c_i32, P_i32, P_i32, P_i32, P_i32, ctypes.POINTER(c_dbl), c_i32,
                                      ctypes.c_char_p, ctypes.c_size_t, P_i32]
     for name in EXPORTS:

@@ -122,7 +122,8 @@ class PHEngine:
         _track(self)
         # library calls of the PH step, by kind (tests assert which path a loop took)
         self.calls = {"ph_reduce": 0, "ph_update_ex": 0, "ph_step_local": 0, "ph_step_defer": 0,
-                      "allreduce_xbar": 0, "allreduce_conv_side": 0, "allreduce_conv_main": 0, "xbar_ahead_used": 0}
+                      "allreduce_xbar": 0, "allreduce_conv_side": 0, "allreduce_conv_main": 0, "xbar_ahead_used": 0,
+                      "ph_loop": 0}
         # several ranks: the conv all-reduce on a side stream under the next solve (False: on
         # the launch stream ahead of it -- bench.py --no-conv-overlap, the comparison case)
         self.overlap_conv = True
@@ -484,6 +485,39 @@ class PHEngine:
         if st is None:  # a later launch replaced the library's statistics: count statuses
             return self.count_not_optimal()
         return int(st[1:4].sum())
+
+    def ph_loop(self, options, max_iters, convthresh):
+        """PHBase.iterk_loop of one rank in one launch (phgpu_ph_loop): up to ``max_iters``
+        iterations of x̄ -> W -> conv -> (conv < convthresh: stop) -> solve, on the current
+        output set, W, x̄ and node_buf.  Returns {"steps", "end", "ipm_iters", "conv",
+        "ms"} -- end 0: the iteration limit, 1: converged, 2: a solve handed scenarios to the
+        PDHG fallback (solved; the caller goes on step by step) -- or None when the handle's
+        state is not one the loop runs (nothing launched)."""
+        if self.comm.size != 1:
+            return None
+        self._flush_step()
+        self._xbar_pending = False          # the loop computes x̄ from x itself
+        self._ahead_id = 0
+        conv = np.zeros(max(1, int(max_iters)), dtype=np.float64)
+        out = np.zeros(4, dtype=np.int64)
+        self._launch_id += 1
+        self._cur_id = self._launch_id
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        rc = self.lib.phgpu_ph_loop(self.h, ctypes.byref(options), int(max_iters), float(convthresh), _ptr(self.x),
+                                    _ptr(self.y if self.want_duals else None), _ptr(self.obj), _ptr(self.bound),
+                                    _ptr(self.status), _ptr(self.iters), _ptr(self.node_buf),
+                                    conv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), self._stream())
+        if rc == -3:
+            return None
+        _lib.check(rc, "phgpu_ph_loop")
+        ev[1].record()
+        ev[1].synchronize()
+        self.calls["ph_loop"] += 1
+        steps = int(out[0])
+        return {"steps": steps, "end": int(out[1]), "ipm_iters": int(out[2]), "conv": conv[:steps].tolist(),
+                "ms": ev[0].elapsed_time(ev[1])}
 
     def compute_xbar_partials(self):
         self.calls["ph_reduce"] += 1

@@ -282,6 +282,17 @@ class PHBase(SPOpt):
             return False
         return True
 
+    def _fused_loop(self, have_ext):
+        """The whole loop in one launch (engine.ph_loop) when nothing but the
+        convergence test decides between the iterations: one rank, no extension, converger or
+        spoke, no progress / timing display -- the state the speculative solve needs plus
+        those.  options["fused_ph_loop"] = False turns it off."""
+        if not self.options.get("fused_ph_loop", True) or self.n_proc > 1 or self.spcomm is not None:
+            return False
+        if have_ext or self.options.get("display_progress") or self.options.get("display_convergence_detail"):
+            return False
+        return self._speculate(have_ext)
+
     def iterk_loop(self):
         verbose = self.options["verbose"]
         have_ext = self.extensions is not None
@@ -290,7 +301,37 @@ class PHBase(SPOpt):
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.converged = False
-        for self._PHIter in range(1, max_iterations + 1):
+        first = 1
+        if max_iterations >= 1 and self._fused_loop(have_ext):
+            t0 = time.perf_counter()
+            r = self.engine.ph_loop(self._to_phgpu_options(self.current_solver_options), max_iterations,
+                                    float(self.options["convthresh"]))
+            if r is not None:
+                steps = r["steps"]
+                self.fused_loops = getattr(self, "fused_loops", []) + [r]
+                dt = (time.perf_counter() - t0) / max(1, steps)
+                self.iter_times.extend([dt] * steps)
+                self._PHIter = steps
+                self.conv = r["conv"][-1] if steps else None
+                if r["end"] == 1:
+                    self.converged = True
+                    global_toc("Convergence metric=%f dropped below user-supplied threshold=%f"
+                               % (self.conv, self.options["convthresh"]), self.cylinder_rank == 0)
+                    self.gripe_report()
+                    return
+                if r["end"] == 0:
+                    if self.engine.count_not_optimal() > 0:
+                        self._gripe_print()
+                    self.mpicomm.Barrier()
+                    global_toc("Reached user-specified limit=%d on number of PH iterations" % max_iterations,
+                               self.cylinder_rank == 0)
+                    return
+                # a solve handed scenarios to the PDHG fallback (solved after the launch): the
+                # remaining iterations run one by one
+                if self.engine.count_not_optimal() > 0:
+                    self._gripe_print()
+                first = steps + 1
+        for self._PHIter in range(first, max_iterations + 1):
             t0 = time.perf_counter()
             if dprogress:
                 global_toc(f"\nInitiating PH Iteration {self._PHIter}\n", self.cylinder_rank == 0)

@@ -46,19 +46,22 @@ def _record_conv(ph):
     return seen
 
 
-@pytest.mark.parametrize("path,eps_rel,w_tol", [(6, 1e-9, ABS), (2, 1e-9, 1e-4), (2, 1e-10, ABS)])
-def test_config3_iterations_to_convergence(gpu, path, eps_rel, w_tol):
+@pytest.mark.parametrize("path,eps_rel,w_tol,fused", [(6, 1e-9, ABS, True), (6, 1e-9, ABS, False), (2, 1e-9, 1e-4, False),
+                                                      (2, 1e-10, ABS, False)])
+def test_config3_iterations_to_convergence(gpu, path, eps_rel, w_tol, fused):
     """eps_rel 1e-9 is the bench's PH-subproblem tolerance: iterations, conv and x̄ meet
     the north_star bars, W (the sum of 1,078 solves' rho (x - x̄)) stays within 1e-4 of
     the exact oracle (4.7e-5 measured on one of 1,024 sampled scenarios, ~3e-7 typical);
     with the subproblems at 1e-10 W meets 1e-5 too.  Path 6 (the interior point, the
     default for this pattern since round 3) presses each solve to 1e-13 and meets 1e-5 at
-    the bench's 1e-9; path 2 (the register PDHG) runs with PHGPU_IPM=0."""
+    the bench's 1e-9; path 2 (the register PDHG) runs with PHGPU_IPM=0.  Path 6 runs twice:
+    the whole loop in one launch (fused: phgpu_ph_loop, the bench's one-rank loop since round
+    6) and step by step (the speculative solve with the step folded into its launch)."""
     keep = os.environ.get("PHGPU_IPM")
     if path == 2:
         os.environ["PHGPU_IPM"] = "0"
     try:
-        _run_convergence(path, eps_rel, w_tol)
+        _run_convergence(path, eps_rel, w_tol, fused)
     finally:
         if keep is None:
             os.environ.pop("PHGPU_IPM", None)
@@ -66,14 +69,14 @@ def test_config3_iterations_to_convergence(gpu, path, eps_rel, w_tol):
             os.environ["PHGPU_IPM"] = keep
 
 
-def _run_convergence(path, eps_rel, w_tol):
+def _run_convergence(path, eps_rel, w_tol, fused=False):
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     S = CONV["S"]
     names = farmer.scenario_names_creator(S)
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 1500, "defaultPHrho": 1.0, "convthresh": 1e-3,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
-            "batch_creator": farmer.batch_creator,
+            "batch_creator": farmer.batch_creator, "fused_ph_loop": fused,
             "iterk_solver_options": {**farmer.PDHG_ITERK_OPTIONS, "eps_rel": eps_rel}}
     ph = PH(opts, names, farmer.scenario_creator, scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": S})
     ph.PH_Prep()
@@ -89,7 +92,13 @@ def _run_convergence(path, eps_rel, w_tol):
     seen = _record_conv(ph)
     ph.iterk_loop()
     assert ph._speculate(False), "the bench's loop variant (speculative solve) must be the one tested"
-    if path == 6:
+    if fused:
+        # one launch for the whole loop: its conv record is the trajectory
+        assert ph.engine.calls["ph_loop"] == 1 and len(ph.fused_loops) == 1, ph.engine.calls
+        assert not seen
+        seen = list(ph.fused_loops[0]["conv"])
+        assert ph.fused_loops[0]["end"] == 1
+    elif path == 6:
         # the bench's exact variant: the one-rank PH step folded into the one-lane solve
         # launch on every iteration that solved
         ii = ph.engine.ipm_info()

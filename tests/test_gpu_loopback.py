@@ -51,6 +51,7 @@ def _run(share, size, comm, iters, convthresh=-1.0):
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": iters, "defaultPHrho": 1.0, "convthresh": convthresh,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
             "batch_creator": farmer.batch_creator, "iter0_solver_options": {"eps_rel": 1e-9},
+            "fused_ph_loop": False,  # (the step-by-step one-rank loop is the comparison)
             "iterk_solver_options": {"eps_rel": 1e-9}}
     kw = {"crops_multiplier": 1, "num_scens": share * size if comm is not None else share}
     ph = PH(opts, names, farmer.scenario_creator, scenario_creator_kwargs=kw, mpicomm=comm)

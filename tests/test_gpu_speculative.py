@@ -30,7 +30,7 @@ def _farmer(S, spec, thresh, kernel=0, cm=1):
     so = {"kernel": kernel} if kernel else {}
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 2000, "defaultPHrho": 1.0, "convthresh": thresh,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
-            "batch_creator": farmer.batch_creator, "speculative_solve": spec,
+            "batch_creator": farmer.batch_creator, "speculative_solve": spec, "fused_ph_loop": False,
             "iter0_solver_options": dict(so), "iterk_solver_options": dict(so)}
     return PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
               scenario_creator_kwargs={"crops_multiplier": cm, "num_scens": S})
@@ -45,7 +45,7 @@ def _aircond(spec, thresh):
           "sigma_dev": 40, "start_seed": 0}
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 2000, "defaultPHrho": 1.0, "convthresh": thresh,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
-            "batch_creator": aircond.batch_creator, "speculative_solve": spec}
+            "batch_creator": aircond.batch_creator, "speculative_solve": spec, "fused_ph_loop": False}
     return PH(opts, aircond.scenario_names_creator(24), aircond.scenario_creator, scenario_creator_kwargs=kw,
               all_nodenames=create_nodenames_from_branching_factors(bf))
 

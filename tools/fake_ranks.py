@@ -57,7 +57,7 @@ def run(size, steps, comm):
         names = names[:S // size]
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": -1.0,
             "verbose": False, "display_progress": False, "toc": False, "device": "cuda:0",
-            "batch_creator": farmer.batch_creator, "iterk_solver_options": {"beta_sufficient": 0.6},
+            "batch_creator": farmer.batch_creator, "fused_ph_loop": False, "iterk_solver_options": {"beta_sufficient": 0.6},
             "iter0_solver_options": {"eps_rel": 1e-9}}
     # (the one-rank run on the share: probabilities 1/share, the same scenario data)
     kw = {"crops_multiplier": 1, "num_scens": S if comm is not None else S // size}
