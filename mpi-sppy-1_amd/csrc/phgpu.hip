@@ -2829,6 +2829,39 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
     return 0;
 }
 
+// Once per scenario data: does any wave span two nodes (xbar_mixed), is every nonant on one
+// node (xbar_single), and the node_buf index of each nonant for the folded PH step (nb_idx)
+static int xbar_layout(phgpu_state* h, hipStream_t st) {
+    if (h->xbar_mixed >= 0) return 0;
+    int32_t* d = nullptr;
+    int32_t v[2] = {0, 0};
+    HIPCHK(hipMalloc((void**)&d, 2 * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(d, 0, 2 * sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_xbar_mixed, grid_for(h->S), dim3(BLOCK), 0, st, *h, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(v, d, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipFree(d));
+    h->xbar_mixed = v[0] ? 1 : 0;
+    h->xbar_single = v[1] ? 0 : 1;
+    if (h->xbar_single && h->nn > 0 && h->nn <= XL_NN_MAX && !h->nb_idx) {
+        // node_buf index of each nonant (its one node, offset) for the folded PH step
+        std::vector<int32_t> dep(h->nn), off(h->nn), idx(h->nn);
+        HIPCHK(hipMemcpy(dep.data(), h->nonant_depth, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(off.data(), h->nonant_off, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int k = 0; k < h->nn; ++k) {
+            int32_t g = 0;
+            HIPCHK(hipMemcpy(&g, h->node_of + (size_t)dep[k] * h->S, sizeof(int32_t), hipMemcpyDeviceToHost));
+            idx[k] = g * h->nlen_max + off[k];
+        }
+        int32_t* di = nullptr;
+        HIPCHK(hipMalloc((void**)&di, h->nn * sizeof(int32_t)));
+        HIPCHK(hipMemcpy(di, idx.data(), h->nn * sizeof(int32_t), hipMemcpyHostToDevice));
+        h->nb_idx = di;
+    }
+    return 0;
+}
+
 // The PH loop of one rank in one cooperative launch (include/phgpu.h, solve_ipm.inc's
 // IPM_LOOP module)
 extern "C" int phgpu_ph_loop(phgpu_handle h, const phgpu_options* opt, int max_iters, double convthresh,
@@ -2838,6 +2871,10 @@ extern "C" int phgpu_ph_loop(phgpu_handle h, const phgpu_options* opt, int max_i
     if (max_iters < 1) return set_err(-1, "phgpu_ph_loop: max_iters must be >= 1");
     FLUSH_STEP(h);
     hipStream_t st = (hipStream_t)stream;
+    {
+        const int rc = xbar_layout(h, st);  // (known after the first phgpu_ph_reduce otherwise)
+        if (rc) return rc;
+    }
     const int why = ph_loop_eligible(h);
     if (why) return set_err(-3, "phgpu_ph_loop: not eligible (reason %d); run the PH steps one by one", why);
     phgpu_options o;
@@ -3057,33 +3094,9 @@ extern "C" int phgpu_solve_stats(phgpu_handle h, int64_t* out, void* stream) {
 // the x̄ partial sums of phgpu_ph_reduce (node_buf cleared, per-wave partials in part)
 static int xbar_partials(phgpu_state* h, const double* x, double* node_buf, hipStream_t st) {
     const size_t nb = (size_t)2 * h->num_nodes * h->nlen_max;
-    if (h->xbar_mixed < 0) {  // once per scenario data: does any wave span two nodes?
-        int32_t* d = nullptr;
-        int32_t v[2] = {0, 0};
-        HIPCHK(hipMalloc((void**)&d, 2 * sizeof(int32_t)));
-        HIPCHK(hipMemsetAsync(d, 0, 2 * sizeof(int32_t), st));
-        hipLaunchKernelGGL(k_xbar_mixed, grid_for(h->S), dim3(BLOCK), 0, st, *h, d);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(v, d, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        HIPCHK(hipFree(d));
-        h->xbar_mixed = v[0] ? 1 : 0;
-        h->xbar_single = v[1] ? 0 : 1;
-        if (h->xbar_single && h->nn > 0 && h->nn <= XL_NN_MAX && !h->nb_idx) {
-            // node_buf index of each nonant (its one node, offset) for the folded PH step
-            std::vector<int32_t> dep(h->nn), off(h->nn), idx(h->nn);
-            HIPCHK(hipMemcpy(dep.data(), h->nonant_depth, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(off.data(), h->nonant_off, h->nn * sizeof(int32_t), hipMemcpyDeviceToHost));
-            for (int k = 0; k < h->nn; ++k) {
-                int32_t g = 0;
-                HIPCHK(hipMemcpy(&g, h->node_of + (size_t)dep[k] * h->S, sizeof(int32_t), hipMemcpyDeviceToHost));
-                idx[k] = g * h->nlen_max + off[k];
-            }
-            int32_t* di = nullptr;
-            HIPCHK(hipMalloc((void**)&di, h->nn * sizeof(int32_t)));
-            HIPCHK(hipMemcpy(di, idx.data(), h->nn * sizeof(int32_t), hipMemcpyHostToDevice));
-            h->nb_idx = di;
-        }
+    {
+        const int rc = xbar_layout(h, st);
+        if (rc) return rc;
     }
     if (h->xbar_mixed) HIPCHK(hipMemsetAsync(node_buf, 0, nb * sizeof(double), st));
     {

@@ -510,6 +510,7 @@ class PHEngine:
                                     conv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), self._stream())
         if rc == -3:
+            self.ph_loop_declined = _lib.last_error()     # why the state is not one the loop runs
             return None
         _lib.check(rc, "phgpu_ph_loop")
         ev[1].record()
