@@ -325,6 +325,12 @@ int64_t phgpu_workspace_bytes(phgpu_handle h);
  *  of the compiled path-5 kernel, 0 if none is compiled yet}. */
 int phgpu_kernel_info(phgpu_handle h, int32_t* info);
 
+/* Path 4 (shared matrix, PDHG) of the last solve: info[2] = {workgroups per scenario of its
+ * cluster form (0: one workgroup per scenario slot on the queue; K >= 2: a batch smaller
+ * than the GPU, every scenario over K co-resident workgroups with cluster barriers), 1 if
+ * the last solve took path 4}.  No reference counterpart (diagnostics). */
+int phgpu_stream_info(phgpu_handle h, int32_t* info);
+
 /* Path-6 (interior point) diagnostics: info[15] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
  * and 2 if the module failed to compile or load (path 6 is then not the automatic path

@@ -129,8 +129,9 @@ struct phgpu_state {
     // wave w takes cw_slc[cw_ptr[w] .. cw_ptr[w+1]) (rw_* for rows)
     int32_t *cw_ptr, *cw_slc, *rw_ptr, *rw_slc;
     int32_t *sk_iters, *sk_order;  // PDHG iterations of the last solve / longest-first queue order
-    double* split_part;            // grid-sum partials of the split streaming form ([2][blocks][8])
-    int split_blocks;              // its capacity in blocks
+    double* split_part;            // grid-sum partials of the split streaming form ([ncl][2][K][8]) + barriers
+    size_t split_need;             // its size in doubles
+    int last_cluster;              // path 4: workgroups per scenario of the last solve's cluster form (0: none)
     int32_t* sk_bins;              // [2 parities][2][ORDER_BINS] counting-sort histogram / fill counters (path 2)
     int order_parity;              // which half of sk_bins the next register-path solve uses
     int warm_rec;                  // the warm start lives in the records pk (paths 2r, 3), else in x / y
@@ -2562,41 +2563,63 @@ static int solve_impl(phgpu_handle h, const phgpu_options* opt, int warm_start, 
             hipLaunchKernelGGL(k_stream_order, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
         else
             hipLaunchKernelGGL(k_stream_order_identity, dim3((unsigned)((h->S + 255) / 256)), dim3(256), 0, st, *h);
-        if (T > 0) {
-            int occ = 0;
-            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_solve_stream<1, true>, SBLK, 0));
-            // enough waves for one slice each in the longer pass, never more than fit at once
-            int G = (std::max(h->nsl_c, h->nsl_r) + SWAVES - 1) / SWAVES;
-            G = std::min(G, std::max(occ, 1) * h->num_cus);
+        int occ = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_solve_stream<1, true>, SBLK, 0));
+        const int64_t cap = (int64_t)std::max(occ, 1) * h->num_cus;
+        // enough waves for one slice each in the longer pass: no more workgroups per scenario
+        const int kmax = std::max((std::max(h->nsl_c, h->nsl_r) + SWAVES - 1) / SWAVES, 1);
+        // the cluster form for a batch smaller than the GPU (a rank's share of a strong-
+        // scaling run): every scenario over K = capacity / S workgroups at once instead of
+        // one scenario per workgroup on a few CUs (PHGPU_STREAM_CLUSTER=0: off, =K: that K)
+        int Kc = 0;
+        {
+            const char* ce = getenv("PHGPU_STREAM_CLUSTER");
+            const int ask = ce ? atoi(ce) : -1;
+            if (ask != 0 && T == 0) {
+                int64_t k = cap / std::max<int64_t>(h->S, 1);
+                if (ask > 1) k = std::min<int64_t>(ask, k);
+                k = std::min<int64_t>(k, kmax);
+                if (k >= 2) Kc = (int)k;
+            }
+        }
+        if (T > 0 || Kc >= 2) {
+            // the split form: T stragglers over the whole grid (one cluster), or S clusters of Kc
+            const int ncl = Kc >= 2 ? (int)h->S : 1;
+            int G = Kc >= 2 ? (int)h->S * Kc : (int)std::min<int64_t>(kmax, cap);
             G = std::max(G, 1);
-            if (h->split_blocks < G) {
+            const size_t need = (size_t)2 * G * 8 + (size_t)16 * ncl;  // partials, then 128-B barrier counters
+            if (h->split_need < need) {
                 if (h->split_part) HIPCHK(hipFree(h->split_part));
                 h->split_part = nullptr;
-                // partials [2][G][8], then the barrier counter
-                HIPCHK(hipMalloc((void**)&h->split_part, (size_t)(2 * G * 8 + 1) * sizeof(double)));
-                h->split_blocks = G;
+                HIPCHK(hipMalloc((void**)&h->split_part, need * sizeof(double)));
+                h->split_need = need;
             }
-            // the barrier counter starts at gbase (PHGPU_SPLIT_BAR_BASE: a test starts it just
-            // below 2^32 so that it wraps during the launch; the barrier compares wrap-safe)
+            // the barrier counters start at gbase (PHGPU_SPLIT_BAR_BASE: a test starts them just
+            // below 2^32 so that they wrap during the launch; the barrier compares wrap-safe)
             const char* bbe = getenv("PHGPU_SPLIT_BAR_BASE");
             unsigned gbase = bbe ? (unsigned)strtoul(bbe, nullptr, 0) : 0u;
-            HIPCHK(hipMemsetAsync(h->split_part + (size_t)2 * G * 8, 0, sizeof(double), st));
-            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(h->split_part + (size_t)2 * G * 8), (int)gbase, 1, st));
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(h->split_part + (size_t)2 * G * 8), (int)gbase, (size_t)32 * ncl, st));
             phgpu_state hv = *h;
             int32_t* qh = h->qhead;
             double* gp = h->split_part;
-            int q0 = T;
-            void* args[] = {&hv, &P, &qh, &x, &y, &obj, &bound, &status, &iters, &q0, &gp, &gbase};
+            int q0 = Kc >= 2 ? (int)h->S : T;
+            int nc = ncl;
+            void* args[] = {&hv, &P, &qh, &x, &y, &obj, &bound, &status, &iters, &q0, &gp, &gbase, &nc};
             HIPCHK(hipLaunchCooperativeKernel((const void*)k_solve_stream<1, true>, dim3((unsigned)G), dim3(SBLK), args,
                                               0, st));
+            h->last_cluster = Kc >= 2 ? Kc : 0;
+        } else {
+            h->last_cluster = 0;
         }
-        nblk = std::min<int64_t>(nblk, std::max<int64_t>((h->S - T + B - 1) / B, 1));
-        if (B == 1)
-            hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters, T, (double*)nullptr, 0u);
-        else
-            hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
-                               bound, status, iters, T, (double*)nullptr, 0u);
+        if (Kc < 2) {
+            nblk = std::min<int64_t>(nblk, std::max<int64_t>((h->S - T + B - 1) / B, 1));
+            if (B == 1)
+                hipLaunchKernelGGL(k_solve_stream<1>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+                                   bound, status, iters, T, (double*)nullptr, 0u, 1);
+            else
+                hipLaunchKernelGGL(k_solve_stream<2>, dim3((unsigned)nblk), dim3(SBLK), 0, st, *h, P, h->qhead, x, y, obj,
+                                   bound, status, iters, T, (double*)nullptr, 0u, 1);
+        }
         HIPCHK(hipGetLastError());
         h->last_stats = nullptr;
         h->last_status = status;
@@ -3368,6 +3391,14 @@ extern "C" int phgpu_last_error(char* buf, size_t len) {
 }
 
 extern "C" int64_t phgpu_workspace_bytes(phgpu_handle h) { return h ? h->ws_bytes : -1; }
+
+// path 4 of the last solve (include/phgpu.h)
+extern "C" int phgpu_stream_info(phgpu_handle h, int32_t* info) {
+    if (!h || !info) return set_err(-1, "null argument");
+    info[0] = h->last_path == 4 ? h->last_cluster : 0;
+    info[1] = h->last_path == 4 ? 1 : 0;
+    return 0;
+}
 
 extern "C" int phgpu_kernel_info(phgpu_handle h, int32_t* info) {
     if (!h || !info) return set_err(-1, "null argument");

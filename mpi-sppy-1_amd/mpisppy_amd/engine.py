@@ -231,6 +231,13 @@ class PHEngine:
                 "wg_instance", "wps", "wKC", "wZC", "wKR", "wZR", "path", "rec", "jit_eligible", "jit_wpe"]
         return dict(zip(keys, list(info)))
 
+    def stream_info(self):
+        """Path 4 of the last solve (phgpu_stream_info): workgroups per scenario of its
+        cluster form (0: the queue), whether the last solve took path 4."""
+        info = (ctypes.c_int32 * 2)()
+        _lib.check(self.lib.phgpu_stream_info(self.h, info), "phgpu_stream_info")
+        return {"cluster": int(info[0]), "path4": int(info[1])}
+
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
         info = (ctypes.c_double * 15)()

@@ -294,3 +294,47 @@ def test_uc_ph_subproblems_vs_cpu_interior_point(gpu, eps, obj_rel):
         bound = np.sqrt(2.0 * (np.abs(obj - want) + 2e-6 * np.abs(want))) * 2.0
         assert (dist <= bound).all(), (k, dist, bound)
     e.close()
+
+
+def test_uc_cluster_form_matches_queue(gpu):
+    """A batch smaller than the GPU (a rank's share of a strong-scaling run) runs in the
+    cluster form of the streaming kernel: every scenario over K = capacity / S co-resident
+    workgroups with cluster barriers and cluster sums (phgpu_stream_info).  Against the
+    queue form (PHGPU_STREAM_CLUSTER=0, one workgroup per scenario slot) and HiGHS: the
+    same objectives, cold and warm; the run with the clusters' barrier counters started
+    4,096 below 2^32 (wrapping within the first scenario) is bit-identical to the plain one."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import PHEngine
+    from mpisppy_amd.examples import uc
+    names = GOLD["names"]
+    b = uc.batch_creator(names, num_scens=GOLD["num_scens"])
+    want = np.array(GOLD["lp_obj"])
+    res = {}
+    for mode, env in (("queue", {"PHGPU_STREAM_CLUSTER": "0"}), ("cluster", {}),
+                      ("cluster_wrap", {"PHGPU_SPLIT_BAR_BASE": hex(2**32 - 4096)})):
+        keep = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            e = PHEngine(b, device="cuda:0")
+            assert e.shared and e.kernel_info()["path"] == 4
+            out = []
+            for warm in (False, True):
+                e.solve(_lib.default_options(eps_rel=UC_EPS), warm=warm)
+                info = e.stream_info()
+                assert info["path4"] == 1
+                assert (info["cluster"] >= 2) == (mode != "queue"), (mode, info)
+                st, obj, bnd = e.host("status"), e.host("obj"), e.host("bound")
+                assert (st == _lib.OPTIMAL).all(), (mode, warm, st, e.host("iters"))
+                assert np.all(np.abs(obj - want) <= UC_OBJ_REL * np.abs(want)), (mode, warm, obj, want)
+                assert np.all(np.abs(bnd - want) <= UC_OBJ_REL * np.abs(want)), (mode, warm, bnd, want)
+                out.append((obj.copy(), e.host("x").copy(), e.host("iters").copy()))
+            res[mode] = out
+            e.close()
+        finally:
+            for k, v in keep.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    for (o1, x1, i1), (o2, x2, i2) in zip(res["cluster"], res["cluster_wrap"]):
+        assert np.array_equal(o1, o2) and np.array_equal(x1, x2) and np.array_equal(i1, i2)

@@ -60,9 +60,10 @@ def main():
             src = src[:k] + line + src[k:]
     orig = L.ipm_source
     L.ipm_source = lambda batch, lanes=1: (src, None)  # noqa: E731
-    tk, ts = (int(v) for v in a.trace.split(":")) if a.trace else (-1, -1)
+    tk, ts = (int(v) if v != "all" else -2 for v in a.trace.split(":")) if a.trace else (-1, -1)
     k = src.index("\n", src.index("#define IPM_GAM")) + 1
-    tsrc = src[:k] + f"#define WTRACE(...) if (s == {ts}) printf(__VA_ARGS__)\n" + src[k:]
+    cond = "true" if ts == -2 else f"s == {ts}"
+    tsrc = src[:k] + f"#define WTRACE(...) if ({cond}) printf(__VA_ARGS__)\n" + src[k:]
     try:
         nn = b.nn
         nc = b.nonant_col
@@ -92,11 +93,12 @@ def main():
     for (name, it, st), k in zip(rows, range(len(rows))):
         ok = st == 0
         h = np.bincount(it[ok], minlength=1)
-        tail = " ".join(f"{v}:{h[v]}" for v in range(max(0, len(h) - 6), len(h)) if h[v])
+        tail = " ".join(f"{v}:{h[v]}" for v in range(max(0, len(h) - (99 if os.environ.get("FULLHIST") else 6)), len(h)) if h[v])
         dx = ""
         if ref is not None:
             dx = f"  max|x-ref| {np.abs(xs[k] - ref[k]).max():.2e}"
-        print(f"{name:6s} mean {it[ok].mean():5.2f} max {it[ok].max():3d} fail {int((~ok).sum()):4d}  tail {tail}{dx}")
+        wm = it[: len(it) // 64 * 64].reshape(-1, 64).max(1).mean() if len(it) >= 64 else float(it.max())
+        print(f"{name:6s} mean {it[ok].mean():5.2f} max {it[ok].max():3d} wave-max {wm:5.2f} fail {int((~ok).sum()):4d}  tail {tail}{dx}")
     if a.worst:
         name, it, st = rows[a.worst]
         order = np.argsort(-it)[:8]
