@@ -323,7 +323,7 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir, ipm=None):
         kname = f"k_solve_wg<{kinfo['wKC']}, {kinfo['wZC']}, {kinfo['wKR']}, {kinfo['wZR']}, {kinfo['wps']}>"
         lanes = 64 * kinfo["wps"]
     elif path == 4:
-        return roofline_stream(b, launches, ws_bytes, tag, pdir)
+        return roofline_stream(b, launches, ws_bytes, tag, pdir, kinfo.get("cluster", 0))
     elif path == 6:
         return roofline_ipm(b, ipm, launches, ws_bytes, tag, pdir)
     else:
@@ -361,15 +361,17 @@ def roofline(b, kinfo, launches, ws_bytes, tag, pdir, ipm=None):
     return out
 
 
-def roofline_stream(b, launches, ws_bytes, tag, pdir):
+def roofline_stream(b, launches, ws_bytes, tag, pdir, cluster=0):
     """Roofline of the shared-matrix streaming kernel (path 4): HBM-bound.
     Algorithmic bytes per scenario-iteration = 8 (5n + 4m): X, X0 read and X, U written,
     U read once by the row-pass gathers (n each); Y, Y0 read, Y written and Y read once
     by the column-pass gathers (m each).  The shared matrix and the shared column / row
-    data are L2 / MALL-resident and not counted.  Measured HBM bytes (PMC) alongside."""
+    data are L2 / MALL-resident and not counted.  Measured HBM bytes (PMC) alongside.
+    cluster = K >= 2: a batch smaller than the GPU ran in the cluster form (K workgroups
+    per scenario, k_solve_stream<1, true>)."""
     n, m, nnz = b.n, b.m, b.nnz
     slots = 1 if os.environ.get("PHGPU_STREAM_SLOTS") == "1" else 2      # phgpu_solve's choice
-    kname = f"k_solve_stream<{slots}>"
+    kname = f"k_solve_stream<{slots}>" if cluster < 2 else "k_solve_stream<1, true>"
     launch_ms = float(np.mean([t for t, _ in launches]))
     units = float(np.mean([u for _, u in launches]))
     B = 8 * (5 * n + 4 * m)
@@ -387,7 +389,8 @@ def roofline_stream(b, launches, ws_bytes, tag, pdir):
     return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": B * units,
             "cache_resident": ws_bytes < INFINITY_CACHE, "working_set_bytes": ws_bytes,
-            "kernel": kname, "lanes_per_scenario": 1024 // slots, "launch_ms": launch_ms,
+            "kernel": kname, "lanes_per_scenario": 1024 // slots if cluster < 2 else 1024 * cluster,
+            "workgroups_per_scenario": cluster if cluster >= 2 else None, "launch_ms": launch_ms,
             "scenario_iters_per_launch": units, "bytes_per_scenario_iter": B,
             "flops_per_scenario_iter": 4 * nnz + 10 * n + 6 * m,
             "note": ("achieved = 8 (5n + 4m) bytes x scenario-iterations per launch / mean HIP-event launch "
@@ -737,6 +740,8 @@ def main():
     n_bad = torch.tensor([e.count_not_optimal()], dtype=torch.float64, device=e.device)
     comm.allreduce_sum_(n_bad)
     kinfo = e.kernel_info()
+    if kinfo["path"] == 4:
+        kinfo["cluster"] = e.stream_info()["cluster"]
     ws = e.workspace_bytes() + 8 * (b.S * (b.n + b.m + 3 * max(b.nn, 1) + 4))
     ipm_diag = e.ipm_info()
     rl = roofline(b, kinfo, launches, ws, tag, a.profile_dir, ipm=ipm_diag)

@@ -12,7 +12,7 @@ from mpisppy_amd.examples import uc  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 max_iter = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-b = uc.batch_creator(uc.scenario_names_creator(S), num_scens=1000)
+b = uc.batch_creator(uc.scenario_names_creator(S), num_scens=int(sys.argv[3]) if len(sys.argv) > 3 else 1000)
 e = PHEngine(b, device="cuda:0")
 torch.cuda.synchronize()
 t = time.time()
