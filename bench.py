@@ -381,7 +381,7 @@ def roofline_stream(b, launches, ws_bytes, tag, pdir, cluster=0):
     if pmc:
         try:
             d = json.load(open(pmc))
-            if d.get("kernel") == "void " + kname:
+            if d.get("kernel", "").replace(", false>", ">") == "void " + kname:
                 traffic = d["bytes_per_scenario_iter"]["total_upper"] * units
                 src = os.path.relpath(pmc, ROOT)
         except Exception:

@@ -2,14 +2,15 @@
 # Round 6, pass n: config 5's traffic re-measured on this round's path-4 kernels (PMC
 # FETCH_SIZE / WRITE_SIZE, separate passes, of a cold capped solve: the queue form at 1,000
 # scenarios and the cluster form at the 125-scenario share), then the 1,000-scenario bench
-# line with its CPU baseline and the 125 share's line.
+# line with its CPU baseline and the 125 share's line; first the split / cluster tests and the
+# (pass n2: the 125 share's PMC again, the 1,000 line; two slices per wave trip measured slower.)
 cd "$(dirname "$0")/../.." || exit 1
 O=gpurun_out/r6n
 mkdir -p $O profiles/r06
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 S='import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(round(d["value"],4), "mean_ms", round(d.get("ms_per_step_mean", d["ms_per_step"]),1), "launch", round(r["launch_ms"],1), "frac", r["frac"], "traffic", r.get("traffic"), r.get("kernel"), d["solver_iters_per_ph_iter"], "cpu", (d.get("cpu_baseline") or {}).get("value"))'
-for sc in "1000 2048 1000" "125 2048 125"; do
+for sc in "125 2048 125"; do
   set -- $sc
   cd /tmp
   timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$O/pf$1 -o run -- python3 $R/tools/uc_prof.py $1 $2 $3 > $R/$O/pf$1.log 2>&1 || { echo "pmc fetch $1 failed"; tail -5 $R/$O/pf$1.log; exit 1; }

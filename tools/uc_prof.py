@@ -23,3 +23,4 @@ its = e.host("iters")
 print(f"S={S} solve {dt:.3f}s scenario-iterations {int(its.sum())} max {its.max()} "
       f"-> {dt / its.max() * 1e3:.3f} ms per iteration, {8 * (5 * b.n + 4 * b.m) * its.sum() / dt / 1e9:.0f} GB/s alg",
       flush=True)
+e.close()  # (before the interpreter's teardown: a profiler's exit otherwise finds the handle alive)
