@@ -71,9 +71,9 @@ def parse():
                         "farmer 1,024 cm=10, aircond 32x32x64) and exit non-zero on a mismatch; auto: when "
                         "the workload and rho match a fixture, on: whenever the workload has one (a "
                         "different --rho then fails by design)")
-    p.add_argument("--no-fused-loop", action="store_true",
-                   help="one rank: run PHBase.iterk_loop step by step instead of the fused loop launch "
-                        "(the comparison case)")
+    p.add_argument("--fused-loop", action="store_true",
+                   help="one rank: PHBase.iterk_loop's K iterations in one cooperative launch (phgpu_ph_loop, "
+                        "opt-in: measured no faster than the step-by-step loop, DESIGN.md 3.11)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="scenarios in the CPU sample (0 = auto)")
     p.add_argument("--profile-dir", default=None,
@@ -591,7 +591,7 @@ def main():
     comm = Comm()
     opts = {"solver_name": "mi355x_pdhg", "PHIterLimit": a.warmup, "defaultPHrho": a.rho,
             "convthresh": -1.0, "verbose": False, "display_progress": False, "toc": False,
-            "device": f"cuda:{dev_index}", "fused_ph_loop": not a.no_fused_loop,
+            "device": f"cuda:{dev_index}", "fused_ph_loop": a.fused_loop,
             "iterk_solver_options": {"eps_rel": a.eps}}
     if a.model == "farmer" and not a.default_solver_options:
         # the example's recommended PH-solve options (examples/farmer.py PDHG_ITERK_OPTIONS)

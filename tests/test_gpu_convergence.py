@@ -55,8 +55,8 @@ def test_config3_iterations_to_convergence(gpu, path, eps_rel, w_tol, fused):
     with the subproblems at 1e-10 W meets 1e-5 too.  Path 6 (the interior point, the
     default for this pattern since round 3) presses each solve to 1e-13 and meets 1e-5 at
     the bench's 1e-9; path 2 (the register PDHG) runs with PHGPU_IPM=0.  Path 6 runs twice:
-    the whole loop in one launch (fused: phgpu_ph_loop, the bench's one-rank loop since round
-    6) and step by step (the speculative solve with the step folded into its launch)."""
+    the whole loop in one launch (fused: phgpu_ph_loop, opt-in since round 6) and step by step
+    (the speculative solve with the step folded into its launch, the default)."""
     keep = os.environ.get("PHGPU_IPM")
     if path == 2:
         os.environ["PHGPU_IPM"] = "0"
