@@ -35,6 +35,7 @@
 #define ORDER_BINS 256  // counting-sort bins of the longest-first work queue (solve_reg.inc)
 #define XL_T 1024        // threads per block of k_ph_update_local at most
 #define XL_NN_MAX 16     // nonants per scenario at most for the folded x̄ paths (k_ph_update_local, IPM epilogues)
+#define XL_PF 4          // k_ph_update_local: nonants whose operands are loaded ahead of the x̄ sums
 #define XP_CHUNK_MIN 16  // smallest x̄-partial chunk of the IPM epilogues (256 / 16 lanes)
 
 // ------------------------------------------------------------------ errors
@@ -1303,12 +1304,32 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
     const int half = st.num_nodes * st.nlen_max;
     // every nonant at once: strided loads of the contiguous per-wave partials, wave sums,
     // then the block's waves in order (one barrier)
+    // the scenario's own operands of the first XL_PF nonants, loaded ahead of the x̄ sums
+    // (independent of them; the barrier below would keep them behind)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sc = s < S ? s : S - 1;
+    double xv[XL_PF], wo[XL_PF], rv[XL_PF];
+#pragma unroll
+    for (int k = 0; k < XL_PF; ++k) {
+        const int kk = k < nn ? k : 0;
+        xv[k] = x[(int64_t)st.nonant_col[kk] * S + sc];
+        wo[k] = update_W ? W[(int64_t)kk * S + sc] : 0.0;
+        rv[k] = update_W ? rho[(int64_t)kk * S + sc] : 0.0;
+    }
     double a[XL_NN_MAX], b[XL_NN_MAX];
 #pragma unroll
     for (int k = 0; k < XL_NN_MAX; ++k) a[k] = b[k] = 0.0;
     for (int64_t w = threadIdx.x; w < st.nwaves; w += blockDim.x) {
         const double* pw = st.part + w * nn * 2;
-        if (dirty && dirty[w]) {  // a chunk with a fallback scenario (path-6 partials)
+        // the chunk's flag and partials in flight together (the flag gates the use only)
+        const int dw = dirty ? dirty[w] : 0;
+        double pa[XL_PF], pb[XL_PF];
+#pragma unroll
+        for (int k = 0; k < XL_PF; ++k) {
+            pa[k] = k < nn ? pw[2 * k] : 0.0;
+            pb[k] = k < nn ? pw[2 * k + 1] : 0.0;
+        }
+        if (dw) {  // a chunk with a fallback scenario (path-6 partials)
             for (int k = 0; k < nn; ++k) {
                 double ra, rb;
                 xp_recompute(st, x, w, C, k, ra, rb);
@@ -1321,8 +1342,8 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
 #pragma unroll
         for (int k = 0; k < XL_NN_MAX; ++k)
             if (k < nn) {
-                a[k] += pw[2 * k];
-                b[k] += pw[2 * k + 1];
+                a[k] += k < XL_PF ? pa[k < XL_PF ? k : 0] : pw[2 * k];
+                b[k] += k < XL_PF ? pb[k < XL_PF ? k : 0] : pw[2 * k + 1];
             }
     }
     const int wv = threadIdx.x / WAVE;
@@ -1352,15 +1373,22 @@ k_ph_update_local(phgpu_state st, const double* __restrict__ x, double* __restri
         }
     }
     __syncthreads();
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double acc = 0.0;
     if (s < S) {
-        for (int k = 0; k < nn; ++k) {
+#pragma unroll
+        for (int k = 0; k < XL_PF; ++k)
+            if (k < nn) {
+                const double xb = xbs[k];
+                xbar[IX(k)] = xb;
+                if (update_W) W[IX(k)] = wo[k] + rv[k] * (xv[k] - xb);
+                acc += fabs(xv[k] - xb);
+            }
+        for (int k = XL_PF; k < nn; ++k) {
             const double xb = xbs[k];
-            const double xv = x[IX(st.nonant_col[k])];
+            const double xw = x[IX(st.nonant_col[k])];
             xbar[IX(k)] = xb;
-            if (update_W) W[IX(k)] += rho[IX(k)] * (xv - xb);
-            acc += fabs(xv - xb);
+            if (update_W) W[IX(k)] += rho[IX(k)] * (xw - xb);
+            acc += fabs(xw - xb);
         }
     }
     conv_last_block(acc, o);
