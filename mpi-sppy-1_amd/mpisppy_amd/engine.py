@@ -90,6 +90,7 @@ class PHEngine:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._stream_cache = {}
         b = batch
         S, n, m, nn = b.S, b.n, b.m, b.nn
         self.S, self.n, self.m, self.nn = S, n, m, nn
@@ -191,7 +192,15 @@ class PHEngine:
 
     # -------------------------------------------------------------- plumbing
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the current stream's handle, cached by the stream's identity (torch's
+        # current_stream builds a Stream object per call: ~5 us, twice per PH iteration on
+        # the host's critical path)
+        key = torch._C._cuda_getCurrentStream(self.dev_index)
+        h = self._stream_cache.get(key)
+        if h is None:
+            h = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            self._stream_cache[key] = h
+        return h
 
     def _upload(self):
         _lib.check(self.lib.phgpu_set_scenarios(
