@@ -712,8 +712,15 @@ class PHEngine:
         self._flush_step()          # a deferred step no solve has taken yet: run it now
         a = self._conv_np
         if not self._conv_zero_copy:
-            # several ranks: the side stream's copy is complete once its event is
-            self._conv_ev.synchronize()
+            # several ranks: the side stream's copy is complete once its event is -- polled
+            # (hipEventQuery), not waited on: the blocking wait returned 15-20 us after the
+            # copy had finished, on the host's critical path (loopback trace)
+            ev, n = self._conv_ev, 0
+            while not ev.query():
+                n += 1
+                if n > self._SPIN:
+                    ev.synchronize()
+                    break
             self._conv_seen = max(self._conv_seen, self._conv_seq)
             return float(a[0]) / self.comm.size
         st = self._wait_stats

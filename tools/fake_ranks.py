@@ -67,10 +67,19 @@ def run(size, steps, comm):
     ph.iterk_loop()
     torch.cuda.synchronize()
     ph.options["PHIterLimit"] = steps
+    prof = None
+    if os.environ.get("FAKE_PROF") and comm is not None:  # (cProfile of the timed loop)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     ph.iterk_loop()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof).sort_stats("tottime").print_stats(30)
     its = ph.iter_times[-steps:]
     e = ph.engine
     out = {"local_scenarios": e.S, "median_ms": 1e3 * float(np.median(its[1:])), "mean_ms": 1e3 * el / steps,
