@@ -1211,6 +1211,16 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
     __shared__ double red[XL_T / WAVE];
     __shared__ int last;
     const int wv = threadIdx.x / WAVE, nwb = (int)(blockDim.x / WAVE);
+    // the solve's statistics copies, loaded now by every block's first wave (the previous
+    // launch wrote them: stream order) and reduced only by the last block -- their load is
+    // off the exchange / ticket chain
+    unsigned long long sv[6];
+    {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            sv[k] = (o.stats_dst && t < o.stats_copies) ? o.stats_src[t * PHGPU_STATS_STRIDE + k] : 0ull;
+    }
     const int nblk = (int)(gridDim.x * gridDim.y), bid = (int)(blockIdx.y * gridDim.x + blockIdx.x);
     acc = wave_sum(acc);
     if ((threadIdx.x & (WAVE - 1)) == 0) red[wv] = acc;
@@ -1248,7 +1258,15 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
         for (int u = 0; u < nwb; ++u) t += red[u];
         if (o.stats_dst) {
             unsigned long long v[6];
-            stats_wave(o.stats_src, o.stats_copies, v);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v[k] = sv[k];
+#pragma unroll
+            for (int o2 = 32; o2 > 0; o2 >>= 1)
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const unsigned long long u = __shfl_xor(v[k], o2, 64);
+                    v[k] = k == 5 ? (u > v[k] ? u : v[k]) : v[k] + u;
+                }
             unsigned long long w = v[0];
 #pragma unroll
             for (int k = 1; k < 6; ++k) w = (int)threadIdx.x == k ? v[k] : w;
