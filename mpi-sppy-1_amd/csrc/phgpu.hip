@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <vector>
+#include <mutex>
 #include <map>
 #include <string>
 #include <cctype>
@@ -63,6 +64,7 @@ struct ipm_module;  // solve_ipm.inc: the hipRTC-compiled path-6 module of a han
 
 struct phgpu_state {
     int device;
+    void* rccl;                    // the library's RCCL communicator over the ranks (comm_rccl.inc), or null
     int64_t S;
     int n, m, nnz, nn, depth, num_nodes, nlen_max;
     // shared pattern
@@ -3370,8 +3372,11 @@ extern "C" int phgpu_fix_nonants(phgpu_handle h, const double* xfix, void* strea
     return 0;
 }
 
+#include "comm_rccl.inc"
+
 extern "C" int phgpu_destroy(phgpu_handle h) {
     if (!h) return 0;
+    rccl_release(h);
     g_ipm_tuning_of.erase(h);
     h->pend.active = 0;  // a deferred step that never ran is dropped with the handle
     if (h->oms[0]) {  // the x / y / omega / sk_iters fields may be bound to slot 1: free by slot

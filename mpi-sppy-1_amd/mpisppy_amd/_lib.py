@@ -51,7 +51,8 @@ EXPORTS = ["phgpu_default_options", "phgpu_create", "phgpu_create2", "phgpu_set_
            "phgpu_kernel_info", "phgpu_ipm_info", "phgpu_ipm_source", "phgpu_solve_stats",
            "phgpu_ph_update_ex", "phgpu_ph_step_local", "phgpu_ph_step_defer", "phgpu_ph_step_flush",
            "phgpu_set_nonant_probs", "phgpu_set_ipm_tuning", "phgpu_ipm_prof",
-           "phgpu_ph_loop", "phgpu_stream_info"]
+           "phgpu_ph_loop", "phgpu_stream_info", "phgpu_comm_unique_id", "phgpu_comm_init",
+           "phgpu_allreduce_sum"]
 
 _lib = None
 
@@ -97,6 +98,9 @@ def load(path=None):
     lib.phgpu_workspace_bytes.restype = c_i64
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_stream_info.argtypes = [c_vp, P_i32]
+    lib.phgpu_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.phgpu_comm_init.argtypes = [c_vp, ctypes.c_char_p, c_int, c_int]
+    lib.phgpu_allreduce_sum.argtypes = [c_vp, c_vp, c_i64, c_vp]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
     lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_i64]
     lib.phgpu_ipm_prof.restype = c_i64

@@ -8,6 +8,8 @@ the ROOT-comm Allreduce of convergence_diff (phbase.py:341) and the Ebound /
 Eobjective / E1 / feas_prob sums (spopt.py:341, 386, 404, 435) are all-reduces of
 tiny buffers.  With one rank every call is a no-op.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -32,6 +34,20 @@ class Comm:
         """In-place SUM all-reduce of a tensor (device tensor with RCCL)."""
         if self.size > 1:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def rccl_plan(self):
+        """(nranks, rank) of the RCCL communicator the engine's library opens over these ranks
+        for the PH step's sums (include/phgpu.h phgpu_comm_init), or None to keep them on
+        torch.distributed: the world group on the nccl backend only (PHGPU_NATIVE_RCCL=0
+        turns it off)."""
+        if (self.size > 1 and self.group is None and dist.is_initialized() and dist.get_backend() == "nccl"
+                and os.environ.get("PHGPU_NATIVE_RCCL", "1") != "0"):
+            return self.size, self.rank
+        return None
+
+    def after_native_(self, t):
+        """Hook after a library-issued sum (a loopback communicator scales here)."""
         return t
 
     def allreduce_max_(self, t):

@@ -6,7 +6,9 @@ folded step).  The difference is the multi-rank path's own cost on the GPU and t
 (the reduce / update launches, the side-stream conv copy and its event, the Python
 wrappers), i.e. what an 8-GPU run pays before RCCL's latency.
 
-    python tools/fake_ranks.py [size = 8] [steps = 40]
+    python tools/fake_ranks.py [size = 8] [steps = 40] [loopback | rccl]
+
+``rccl``: the same loopback with a real RCCL all-reduce (a one-rank nccl group) underneath.
 """
 import os
 import sys
@@ -48,7 +50,36 @@ class LoopbackComm:
         return [obj] * self.size
 
 
-def run(size, steps, comm):
+class RcclLoopbackComm(LoopbackComm):
+    """The loopback with a real RCCL all-reduce underneath (a one-rank nccl process group on
+    the same GPU): the engine's multi-rank path then issues RCCL collectives on its launch
+    and side streams exactly as an N-GPU run does; the sum is then scaled by ``size``."""
+
+    def __init__(self, size):
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        self.dist = dist
+        super().__init__(size)
+
+    def allreduce_sum_(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        t.mul_(self.size)
+        return t
+
+    def rccl_plan(self):
+        # the library's own communicator over the one real rank (PHGPU_NATIVE_RCCL=0: torch)
+        return (1, 0) if os.environ.get("PHGPU_NATIVE_RCCL", "1") != "0" else None
+
+    def after_native_(self, t):
+        t.mul_(self.size)
+        return t
+
+
+def run(size, steps, comm, state=False):
     from mpisppy_amd.opt.ph import PH
     from mpisppy_amd.examples import farmer
     S = 65536
@@ -83,7 +114,12 @@ def run(size, steps, comm):
     its = ph.iter_times[-steps:]
     e = ph.engine
     out = {"local_scenarios": e.S, "median_ms": 1e3 * float(np.median(its[1:])), "mean_ms": 1e3 * el / steps,
-           "calls": dict(e.calls), "path": e.kernel_info()["path"], "lanes": e.ipm_info().get("lanes")}
+           "calls": dict(e.calls), "path": e.kernel_info()["path"], "lanes": e.ipm_info().get("lanes"),
+           "native_rccl": bool(getattr(e, "_native", False))}
+    if state:  # (tests: the PH state after the loop)
+        out["conv"] = float(ph.conv)
+        out["W"] = e.host("W").tolist()
+        out["xbar"] = e.host("node_buf").tolist()
     e.close()
     return out
 
@@ -91,6 +127,22 @@ def run(size, steps, comm):
 def main():
     size = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    if len(sys.argv) > 3 and sys.argv[3] == "rccl":  # RCCL collectives under the loopback
+        print(f"rccl (library) loopback {size} ranks:", run(size, steps, RcclLoopbackComm(size)), flush=True)
+        os.environ["PHGPU_NATIVE_RCCL"] = "0"
+        print(f"rccl (torch.distributed) loopback {size} ranks:", run(size, steps, RcclLoopbackComm(size)), flush=True)
+        os.environ.pop("PHGPU_NATIVE_RCCL")
+        print(f"loopback {size} ranks:", run(size, steps, LoopbackComm(size)), flush=True)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "rccl-state":  # (tests/test_gpu_native_rccl.py)
+        import json
+        out = {}
+        for mode in ("library", "torch"):
+            if mode == "torch":
+                os.environ["PHGPU_NATIVE_RCCL"] = "0"
+            out[mode] = run(size, steps, RcclLoopbackComm(size), state=True)
+        print("STATE " + json.dumps(out), flush=True)
+        return
     if len(sys.argv) > 3 and sys.argv[3] == "loopback":  # (under a profiler: that run alone)
         print(f"loopback {size} ranks:", run(size, steps, LoopbackComm(size)), flush=True)
         return
