@@ -329,13 +329,15 @@ int phgpu_kernel_info(phgpu_handle h, int32_t* info);
  * (comm_rccl.inc), in place of the node-communicator Allreduce of _Compute_Xbar and the
  * Allreduce of convergence_diff (phbase.py:83-87, 339-343; mpisppy/MPI.py's Allreduce over
  * mpi4py).  phgpu_comm_unique_id writes a 128-byte RCCL unique id (call it on one rank and
- * broadcast it); phgpu_comm_init joins the handle to the communicator of nranks ranks as
- * rank (collective: every rank calls it); phgpu_allreduce_sum sums n doubles in place over
- * the ranks on stream.  RCCL is loaded at run time (the process's librccl.so.1 or the
- * system's); -2 when it is absent. */
+ * broadcast it); phgpu_comm_init joins the handle's communicator slot (0: the sums issued on
+ * the launch stream, 1: those on a side stream -- one user stream per communicator) to the
+ * communicator of nranks ranks as rank (collective: every rank calls it, one id per slot);
+ * phgpu_allreduce_sum sums n doubles in place over the ranks on stream with the slot's
+ * communicator.  RCCL is loaded at run time (the process's librccl.so.1 or the system's);
+ * -2 when it is absent. */
 int phgpu_comm_unique_id(char* id);
-int phgpu_comm_init(phgpu_handle h, const char* id, int nranks, int rank);
-int phgpu_allreduce_sum(phgpu_handle h, double* buf, int64_t n, void* stream);
+int phgpu_comm_init(phgpu_handle h, const char* id, int nranks, int rank, int slot);
+int phgpu_allreduce_sum(phgpu_handle h, int slot, double* buf, int64_t n, void* stream);
 
 /* Path 4 (shared matrix, PDHG) of the last solve: info[2] = {workgroups per scenario of its
  * cluster form (0: one workgroup per scenario slot on the queue; K >= 2: a batch smaller

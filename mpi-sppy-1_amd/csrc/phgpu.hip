@@ -64,7 +64,7 @@ struct ipm_module;  // solve_ipm.inc: the hipRTC-compiled path-6 module of a han
 
 struct phgpu_state {
     int device;
-    void* rccl;                    // the library's RCCL communicator over the ranks (comm_rccl.inc), or null
+    void* rccl[2];                 // the library's RCCL communicators over the ranks (comm_rccl.inc), or null
     int64_t S;
     int n, m, nnz, nn, depth, num_nodes, nlen_max;
     // shared pattern
@@ -1086,7 +1086,11 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
     int cur = -1, first = -1;
     double a = 0.0, b = 0.0, a_first = 0.0, b_first = 0.0;
     for (int64_t w = w0; w < w1; ++w) {
+        // the chunk's node, dirty flag and partials in flight together (none gates another
+        // load: one memory round trip per chunk instead of three on the x̄ critical path)
         const int gnode = st.part_node[w * st.nn + k];
+        const int dw = dirty ? dirty[w] : 0;
+        const double pa = st.part[(w * st.nn + k) * 2 + 0], pb = st.part[(w * st.nn + k) * 2 + 1];
         if (gnode < 0) continue;
         if (gnode != cur) {
             if (cur >= 0) {
@@ -1103,14 +1107,14 @@ __global__ void __launch_bounds__(XF_THREADS) k_xbar_final(phgpu_state st, doubl
             a = 0.0;
             b = 0.0;
         }
-        if (dirty && dirty[w]) {
+        if (dw) {
             double ra, rb;
             xp_recompute(st, x, w, xpC, k, ra, rb);
             a += ra;
             b += rb;
         } else {
-            a += st.part[(w * st.nn + k) * 2 + 0];
-            b += st.part[(w * st.nn + k) * 2 + 1];
+            a += pa;
+            b += pb;
         }
     }
     if (first < 0) {  // zero or one run in this chunk: it is the first (and last) run

@@ -99,8 +99,8 @@ def load(path=None):
     lib.phgpu_kernel_info.argtypes = [c_vp, P_i32]
     lib.phgpu_stream_info.argtypes = [c_vp, P_i32]
     lib.phgpu_comm_unique_id.argtypes = [ctypes.c_char_p]
-    lib.phgpu_comm_init.argtypes = [c_vp, ctypes.c_char_p, c_int, c_int]
-    lib.phgpu_allreduce_sum.argtypes = [c_vp, c_vp, c_i64, c_vp]
+    lib.phgpu_comm_init.argtypes = [c_vp, ctypes.c_char_p, c_int, c_int, c_int]
+    lib.phgpu_allreduce_sum.argtypes = [c_vp, c_int, c_vp, c_i64, c_vp]
     lib.phgpu_ipm_info.argtypes = [c_vp, ctypes.POINTER(c_dbl)]
     lib.phgpu_ipm_prof.argtypes = [c_vp, ctypes.POINTER(ctypes.c_ulonglong), c_i64]
     lib.phgpu_ipm_prof.restype = c_i64

@@ -202,19 +202,26 @@ class PHEngine:
         if plan is None:
             return
         nranks, rank = plan
-        uid = ctypes.create_string_buffer(128)
+        # two communicators: the launch stream's x̄ sums (slot 0) and the side stream's conv
+        # sums (slot 1), so that neither alternates between streams
+        ids = [ctypes.create_string_buffer(128) for _ in range(2)]
         if rank == 0:
-            _lib.check(self.lib.phgpu_comm_unique_id(uid), "phgpu_comm_unique_id")
-        raw = self.comm.bcast_object(uid.raw if rank == 0 else None, root=0) if nranks > 1 else uid.raw
-        uid = ctypes.create_string_buffer(bytes(raw), 128)
-        _lib.check(self.lib.phgpu_comm_init(self.h, uid, int(nranks), int(rank)), "phgpu_comm_init")
+            for u in ids:
+                _lib.check(self.lib.phgpu_comm_unique_id(u), "phgpu_comm_unique_id")
+        raw = [u.raw for u in ids]
+        if nranks > 1:
+            raw = self.comm.bcast_object(raw if rank == 0 else None, root=0)
+        for slot in (0, 1):
+            u = ctypes.create_string_buffer(bytes(raw[slot]), 128)
+            _lib.check(self.lib.phgpu_comm_init(self.h, u, int(nranks), int(rank), slot), "phgpu_comm_init")
         self._native = True
 
-    def _ar(self, t):
-        """In-place sum of a device fp64 tensor over the ranks."""
+    def _ar(self, t, tag="critical"):
+        """In-place sum of a device fp64 tensor over the ranks (tag "overlapped": the side
+        stream's conv sum, on the library's second communicator)."""
         if self._native and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous():
-            _lib.check(self.lib.phgpu_allreduce_sum(self.h, _ptr(t), int(t.numel()), self._stream()),
-                       "phgpu_allreduce_sum")
+            _lib.check(self.lib.phgpu_allreduce_sum(self.h, 1 if tag == "overlapped" else 0, _ptr(t),
+                                                    int(t.numel()), self._stream()), "phgpu_allreduce_sum")
             return self.comm.after_native_(t)
         return self.comm.allreduce_sum_(t)
 
@@ -429,15 +436,15 @@ class PHEngine:
         all-reduce on the side stream)."""
         ins = getattr(self, "_ins", None)
         if ins is None or self.comm.size == 1 or not self._recording():
-            return self._ar(t)
+            return self._ar(t, tag)
         # the first _AR_TIMED all-reduces are timed (each event record is a marker packet
         # that idles the GPU ~5.6 us); the rest are counted and the mean extrapolated
         ins["ar_count"] += 1
         if len(ins["ar_events"]) >= self._AR_TIMED:
-            return self._ar(t)
+            return self._ar(t, tag)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-        self._ar(t)
+        self._ar(t, tag)
         ev[1].record()
         ins["ar_events"].append((ev, tag))
         return t
