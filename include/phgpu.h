@@ -345,7 +345,7 @@ int phgpu_allreduce_sum(phgpu_handle h, int slot, double* buf, int64_t n, void* 
  * the last solve took path 4}.  No reference counterpart (diagnostics). */
 int phgpu_stream_info(phgpu_handle h, int32_t* info);
 
-/* Path-6 (interior point) diagnostics: info[15] = {1 if path 6 applies to the pattern,
+/* Path-6 (interior point) diagnostics: info[16] = {1 if path 6 applies to the pattern,
  * factor entries of the pattern with every row active, 1 if a compiled module spilled
  * and 2 if the module failed to compile or load (path 6 is then not the automatic path
  * until new data arrives by phgpu_set_scenarios), 1 if a module is compiled, rows in its normal
@@ -356,7 +356,9 @@ int phgpu_stream_info(phgpu_handle h, int32_t* info);
  * steps folded into solve launches so far (phgpu_ph_step_defer), the IPM kernel (0 none
  * compiled, 1 one lane, 2 lane groups, 3 workgroup, 4 subtree), and of the last path-6 solve
  * (synchronises): scenarios the subtree kernel found still jammed after its re-centrings
- * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings}. */
+ * (handed to the PDHG fallback, never reported OPTIMAL), re-centrings, and 1 when the
+ * one-lane module keeps its slack reciprocals in LDS (a module that spilled otherwise,
+ * PHGPU_IPM_LDS=0 turns it off)}: 16 doubles. */
 int phgpu_ipm_info(phgpu_handle h, double* info);
 
 /* PHBase.iterk_loop (phbase.py:875-979) of one rank in one cooperative launch (no

@@ -178,6 +178,10 @@ struct phgpu_state {
     int64_t loop_dbl_n;
     unsigned long long* loop_cnt;
     int ipm_flags_valid, ipm_nf, ipm_off, ipm_parity, ipm_spill1;
+    // the one-lane module's slack reciprocals in LDS (IPM_LDS_ISL, solve_ipm.inc ipm_prepare):
+    // 0 not tried, 1 on (its module spills less), -1 tried and not kept; with the spill
+    // bytes of the register-only module it was compared with
+    int ipm_lds, ipm_lds_ref;
     int ipm_wave;  // waves per scenario of the workgroup IPMs for medium scenarios (0: not eligible;
                    // jit_ipm_blk.hip.in for block-angular patterns, else jit_ipm_wave.hip.in)
     int32_t *ipm_list, *ipm_cnt;
@@ -2462,6 +2466,7 @@ extern "C" int phgpu_set_scenarios(phgpu_handle h, const double* A_val, const do
     h->ipm_flags_valid = 0;
     h->ipm_off = 0;
     h->ipm_spill1 = 0;
+    h->ipm_lds = 0;
     bind_slots(h);
     HIPCHK(run_setup(h, st));
     // the setup's start omega (slot 0) for slot 1 too
@@ -3503,7 +3508,7 @@ extern "C" int64_t phgpu_ipm_prof(phgpu_handle h, unsigned long long* out, int64
 
 extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
     if (!h || !info) return set_err(-1, "null argument");
-    for (int k = 0; k < 15; ++k) info[k] = 0.0;
+    for (int k = 0; k < 16; ++k) info[k] = 0.0;
     info[0] = ipm_eligible(h) ? 1.0 : 0.0;
     info[11] = (double)h->folded;
     info[1] = h->ipm_nf;
@@ -3518,6 +3523,7 @@ extern "C" int phgpu_ipm_info(phgpu_handle h, double* info) {
         info[9] = h->ipm->sol_flops;
         info[10] = h->ipm->L;
         info[12] = h->ipm->L == 1 ? 1 : (h->ipm->L < 64 ? 2 : (h->ipm->blk ? 4 : 3));
+        info[15] = h->ipm->L == 1 && h->ipm_lds == 1 ? 1.0 : 0.0;
     }
     // the subtree kernel's jam statistics of the last path-6 solve (synchronous read)
     if (h->last_stats && h->ipm_stats && h->last_path == 6) {

@@ -283,10 +283,11 @@ class PHEngine:
 
     def ipm_info(self):
         """Path 6 (interior point) of the handle (phgpu_ipm_info)."""
-        info = (ctypes.c_double * 15)()
+        info = (ctypes.c_double * 16)()
         _lib.check(self.lib.phgpu_ipm_info(self.h, info), "phgpu_ipm_info")
         keys = ["eligible", "nf_bound", "off", "compiled", "rows", "factor_entries", "scratch_bytes", "compile_s",
-                "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel", "jam_handovers", "recentrings"]
+                "factor_flops", "solve_flops", "lanes", "folded_steps", "kernel", "jam_handovers", "recentrings",
+                "lds_slacks"]
         return dict(zip(keys, list(info)))
 
     def ipm_prof(self):

@@ -95,26 +95,38 @@ def test_aircond432_on_the_path2_instance(gpu, pinned_l8_record_mode):
         assert np.abs(nx[nd][:2] - np.array(v)).max() <= 1e-4, nd
 
 
-def _assert_path6(ph):
+def _assert_path6(ph, lds=True):
     """The bench's config-4 instance: path 6 (interior point), one lane per scenario at
-    65,536 scenarios (its module spills 524 B per lane, below IPM_SPILL_MAX: faster than
-    lane groups of 4)."""
+    65,536 scenarios.  Its register-only module spills 516 B per lane (below IPM_SPILL_MAX:
+    faster than lane groups of 4); with the slack reciprocals in LDS (the
+    automatic choice for a module that spills, solve_ipm.inc ipm_prepare) 132 B."""
     info = ph.engine.kernel_info()
     assert info["path"] == 6, info
     ipm = ph.engine.ipm_info()
     assert ipm["compiled"] == 1 and ipm["off"] == 0 and ipm["scratch_bytes"] <= 1024, ipm
     assert int(ipm["lanes"]) == 1, ipm
+    assert int(ipm["lds_slacks"]) == int(lds), ipm
+    if lds:
+        assert ipm["scratch_bytes"] <= 256, ipm
 
 
-@pytest.fixture(params=["path6", "path2"])
+def _assert_path6_regs(ph):
+    _assert_path6(ph, lds=False)
+
+
+@pytest.fixture(params=["path6", "path6_regs", "path2"])
 def config4_path(request):
-    """path6: the automatic choice (what bench.py runs); path2: PHGPU_IPM=0, the register
-    PDHG kernel <3,3,1,4>, L = 8, record mode."""
-    keep = {k: os.environ.get(k) for k in ("PHGPU_IPM",)}
+    """path6: the automatic choice (what bench.py runs); path6_regs: PHGPU_IPM_LDS=0, the
+    register-only module (slack reciprocals in registers and scratch); path2: PHGPU_IPM=0,
+    the register PDHG kernel <3,3,1,4>, L = 8, record mode."""
+    keep = {k: os.environ.get(k) for k in ("PHGPU_IPM", "PHGPU_IPM_LDS")}
+    os.environ.pop("PHGPU_IPM_LDS", None)
     if request.param == "path2":
         os.environ["PHGPU_IPM"] = "0"
     else:
         os.environ.pop("PHGPU_IPM", None)
+    if request.param == "path6_regs":
+        os.environ["PHGPU_IPM_LDS"] = "0"
     yield request.param
     for k, v in keep.items():
         if v is None:
@@ -125,7 +137,7 @@ def config4_path(request):
 
 @pytest.mark.skipif(not os.path.exists(SCALE_FILE), reason="aircond_scale.json not generated")
 def test_config4_aircond65536_vs_oracle(gpu, config4_path):
-    check = _assert_path6 if config4_path == "path6" else _assert_path2_instance
+    check = {"path6": _assert_path6, "path6_regs": _assert_path6_regs}.get(config4_path, _assert_path2_instance)
     g = json.load(open(SCALE_FILE))
     assert g["kwargs"] == KW and g["rho"] == 1.0
     ph = _aircond_ph(g["branching_factors"], g["ph_iters"], -1.0)
