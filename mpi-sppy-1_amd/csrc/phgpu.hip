@@ -1290,26 +1290,50 @@ __device__ __forceinline__ void conv_last_block(double acc, const conv_sink& o) 
 // phbase.py:90-103 (scatter x̄), 293-318 (W update), 330-339 (local |x - x̄| sum, reduced
 // by the last block into conv_local).
 #define UPD_T 256
+#define UPD_BLOCKS 256  // at most about this many blocks: each takes a ticket on one counter
+#define UPD_U 4         // scenarios per thread in flight per trip
 __global__ void __launch_bounds__(UPD_T)
 k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restrict__ node_buf,
             double* __restrict__ xbar, double* __restrict__ W, const double* __restrict__ rho,
             int update_W, conv_sink o) {
     // one nonant per grid row (blockIdx.y): the per-nonant index loads of a scenario's
     // thread run in parallel instead of one dependent chain per nonant (config 2, 30
-    // nonants: 27 us -> a few)
+    // nonants: 27 us -> a few).  A row's blocks stride over the scenarios (UPD_U loads in
+    // flight per thread), so that the grid stays near UPD_BLOCKS blocks: the last-block
+    // ticket is one atomic counter, and config 4's 1,536 blocks (65,536 scenarios x 6
+    // nonants) queued on it for about 20 us of a 27 us launch
     const int64_t S = st.S;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int k = blockIdx.y;
     double acc = 0.0;
-    if (s < S && k < st.nn) {
+    if (k < st.nn) {
         const int d = st.nonant_depth[k];
-        const int gnode = st.node_of[IX(d)];
-        const double xb = node_buf[gnode * st.nlen_max + st.nonant_off[k]];
-        const double xv = x[IX(st.nonant_col[k])];
-        xbar[IX(k)] = xb;
-        // (variable probabilities: W masked where the probability is 0, phbase.py:315-318)
-        if (update_W) W[IX(k)] = (st.pvar && st.pvar[IX(k)] == 0.0) ? 0.0 : W[IX(k)] + rho[IX(k)] * (xv - xb);
-        acc += fabs(xv - xb);
+        const int off = st.nonant_off[k], col = st.nonant_col[k], nl = st.nlen_max;
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s0 < S; s0 += UPD_U * stride) {
+            double xb[UPD_U], xv[UPD_U], wo[UPD_U], rv[UPD_U];
+            bool pz[UPD_U];
+#pragma unroll
+            for (int u = 0; u < UPD_U; ++u) {
+                const int64_t s = s0 + u * stride;
+                const int64_t sc = s < S ? s : S - 1;
+                const int gnode = st.node_of[(int64_t)d * S + sc];
+                xb[u] = node_buf[gnode * nl + off];
+                xv[u] = x[(int64_t)col * S + sc];
+                wo[u] = update_W ? W[(int64_t)k * S + sc] : 0.0;
+                rv[u] = update_W ? rho[(int64_t)k * S + sc] : 0.0;
+                // (variable probabilities: W masked where the probability is 0, phbase.py:315-318)
+                pz[u] = update_W && st.pvar && st.pvar[(int64_t)k * S + sc] == 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < UPD_U; ++u) {
+                const int64_t s = s0 + u * stride;
+                if (s < S) {
+                    xbar[(int64_t)k * S + s] = xb[u];
+                    if (update_W) W[(int64_t)k * S + s] = pz[u] ? 0.0 : wo[u] + rv[u] * (xv[u] - xb[u]);
+                    acc += fabs(xv[u] - xb[u]);
+                }
+            }
+        }
     }
     conv_last_block(acc, o);
 }
@@ -3262,7 +3286,10 @@ extern "C" int phgpu_ph_update_ex(phgpu_handle h, const double* x, const double*
     const int rc = make_sink(h, conv_local, stats_out, st, o);
     if (rc) return rc;
     // one launch: x̄ scatter, W update, conv (last-block reduction) and the statistics
-    hipLaunchKernelGGL(k_ph_update, dim3((unsigned)((h->S + UPD_T - 1) / UPD_T), (unsigned)std::max(h->nn, 1)), dim3(UPD_T), 0, st, *h, x,
+    // (grid bound measured on config 4, k_ph_update us by kernel trace: 64 blocks 21.1, 128
+    // 14.6, 256 12.9, 512 14.8, unbounded (1,536) 28.2; profiles/r06/ll/)
+    const int64_t bx = std::min<int64_t>((h->S + UPD_T - 1) / UPD_T, std::max<int64_t>(1, UPD_BLOCKS / std::max(h->nn, 1)));
+    hipLaunchKernelGGL(k_ph_update, dim3((unsigned)bx, (unsigned)std::max(h->nn, 1)), dim3(UPD_T), 0, st, *h, x,
                        node_buf, xbar, W, rho, update_W ? 1 : 0, o);
     HIPCHK(hipGetLastError());
     return 0;
