@@ -1315,14 +1315,17 @@ k_ph_update(phgpu_state st, const double* __restrict__ x, const double* __restri
 #pragma unroll
             for (int u = 0; u < UPD_U; ++u) {
                 const int64_t s = s0 + u * stride;
-                const int64_t sc = s < S ? s : S - 1;
-                const int gnode = st.node_of[(int64_t)d * S + sc];
-                xb[u] = node_buf[gnode * nl + off];
-                xv[u] = x[(int64_t)col * S + sc];
-                wo[u] = update_W ? W[(int64_t)k * S + sc] : 0.0;
-                rv[u] = update_W ? rho[(int64_t)k * S + sc] : 0.0;
-                // (variable probabilities: W masked where the probability is 0, phbase.py:315-318)
-                pz[u] = update_W && st.pvar && st.pvar[(int64_t)k * S + sc] == 0.0;
+                xb[u] = xv[u] = wo[u] = rv[u] = 0.0;
+                pz[u] = false;
+                if (s < S) {  // (a wave past S skips its loads: a small batch has one trip of one)
+                    const int gnode = st.node_of[(int64_t)d * S + s];
+                    xb[u] = node_buf[gnode * nl + off];
+                    xv[u] = x[(int64_t)col * S + s];
+                    wo[u] = update_W ? W[(int64_t)k * S + s] : 0.0;
+                    rv[u] = update_W ? rho[(int64_t)k * S + s] : 0.0;
+                    // (variable probabilities: W masked where the probability is 0, phbase.py:315-318)
+                    pz[u] = update_W && st.pvar && st.pvar[(int64_t)k * S + s] == 0.0;
+                }
             }
 #pragma unroll
             for (int u = 0; u < UPD_U; ++u) {
