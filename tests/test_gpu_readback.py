@@ -36,8 +36,9 @@ def _expected_node_buf(e):
 def _engine(model, S, bf=None):
     from mpisppy_amd.engine import PHEngine
     from mpisppy_amd.examples import aircond, farmer
-    if model == "farmer":
-        b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=1, num_scens=S)
+    if model in ("farmer", "farmer10"):  # farmer10: crops_multiplier 10, 30 nonants (config 2)
+        cm = 10 if model == "farmer10" else 1
+        b = farmer.batch_creator(farmer.scenario_names_creator(S), crops_multiplier=cm, num_scens=S)
     else:
         kw = {"branching_factors": bf, "Capacity": 200, "QuadShortCoeff": 0.3, "BeginInventory": 50,
               "mu_dev": 0, "sigma_dev": 40, "start_seed": 0}
@@ -127,6 +128,7 @@ def test_update_ex_rejects_stats_before_solve(gpu):
 
 
 @pytest.mark.parametrize("model,S,bf", [("farmer", 1000, None), ("farmer", 20000, None),
+                                        ("farmer10", 1024, None),   # 30 nonants: the 256-thread kernel
                                         ("aircond", 128, [2, 64])])
 def test_step_local_matches_reduce_then_update(gpu, model, S, bf):
     """phgpu_ph_step_local (one rank: x̄ folded into the update launch for two-stage
